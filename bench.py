@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — primary rays/s of the gfx950 SVO raycaster on BASELINE.json's metric config.
+
+Workload: genWorld's terrain on 4096 x 4096 columns as a depth-12
+(4096^3, 6-level) tree, one 1920x1080 frame of primary rays from (4,90,4) towards
+normalize(1,-0.45,1), step budget 16384, castRayFromCam semantics (every ray ends on terrain).
+A "step" = one frame per GPU: with N ranks, N frames (camera poses shifted along the diagonal)
+are each sharded over all ranks by interleaved 8-pixel tile rows (row r -> rank r mod N), every
+rank casts its rows of every frame, and the hit records are gathered to rank 0 over RCCL.
+Per-GPU work is fixed as N grows ("weak").  Inputs (tree, camera) are resident in HBM before
+the timed region; the timed region is K steps between barrier + synchronize on both sides; the
+reported time is the max over ranks.
+
+Extra objects on the JSON line:
+  roofline     — the cast kernel's algorithmic bytes (B_ray = 16*E_node +
+                 4*E_child + B_out per ray, E from profiles/bray.json) / its average launch time,
+                 measured with HIP events on the launch stream, against the 8 TB/s HBM peak;
+                 traffic = HBM bytes per launch from the committed rocprofv3 PMC pass (or null).
+  cpu_baseline — the oracle's C restatement of castRayFromCam + getBlock (reference layout, full
+                 descent per step) timed on this host's cores on the same frame (rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LEVELS, COLS = 6, 4096
+W, H = 1920, 1080
+ORIGIN = (4.0, 90.0, 4.0)
+CAM = (1.0, -0.45, 1.0)
+STEPS = 16384
+B_OUT = 24  # hit record bytes per ray (int4 pos+steps, f32 t, u32 info)
+
+
+def frame_origin(f):
+    return (ORIGIN[0] + 64.0 * f, ORIGIN[1], ORIGIN[2] + 64.0 * f)
+
+
+def load_bray():
+    p = os.path.join(ROOT, "profiles", "bray.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        c = d.get("C3")
+        if c:
+            return c["e_child_per_ray"], d
+    return None, None
+
+
+def load_traffic():
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        return d.get("hbm_bytes_per_launch"), d
+    return None, None
+
+
+def cpu_baseline(ppx, ppy, gpu_hits=None):
+    """Oracle (test infrastructure) timed on the host: the reference algorithm and layout."""
+    from oracle import oracle as O
+
+    O.build(native=True)
+    cores = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    T = O.Tree.terrain(LEVELS, COLS, COLS, native=True, nthreads=cores)
+    build_s = time.time() - t0
+    dn = O.normalize(CAM)
+    rng = np.random.default_rng(1)
+    pix = np.sort(rng.choice(W * H, W * H // 4, replace=False))
+    t0 = time.time()
+    ref = T.cast_frame(ORIGIN, dn, W, H, STEPS, ppx=ppx, ppy=ppy, pixels=pix, nthreads=cores)
+    dt = time.time() - t0
+    one = pix[:: 64]
+    t1 = time.time()
+    T.cast_frame(ORIGIN, dn, W, H, STEPS, ppx=ppx, ppy=ppy, pixels=one, nthreads=1)
+    dt1 = time.time() - t1
+    res = {
+        "value": len(pix) / dt,
+        "unit": "rays/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": "%d random pixels (1/4) of the same 1080p C3 frame, %d threads; oracle/oracle.c (-O3 -march=native "
+                  "-ffp-contract=off) restating castRayFromCam + getBlock on the reference node/array layout" % (len(pix), cores),
+        "single_thread_rays_per_s": len(one) / dt1,
+        "tree_build_s": round(build_s, 2),
+    }
+    if gpu_hits is not None:
+        g = gpu_hits
+        res["parity_vs_gpu"] = bool(np.array_equal(g["pos"][pix], ref["pos"]) and np.array_equal(g["steps"][pix], ref["steps"]))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cols", type=int, default=COLS)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import raytracing_test_amd as rt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = local
+    torch.cuda.set_device(dev)
+
+    t0 = time.time()
+    tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
+    build_s = time.time() - t0
+    tree.upload(dev)
+    info = tree.info()
+    ppx, ppy = rt.proj_plane(W, H)
+    cam = rt.normalize(CAM)
+
+    nframes = world
+    descs, outs = [], []
+    # equal-size buffers on every rank (RCCL gather): the largest shard's record count
+    max_local = max(rt.Tree.count(rt.Tree.frame_desc(ORIGIN, cam, W, H, STEPS, ppx, ppy, r, world)) for r in range(world))
+    for f in range(nframes):
+        d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world)
+        descs.append(d)
+        outs.append(rt.Tree.alloc_hits(max_local, dev))
+    rays_local = sum(rt.Tree.count(d) for d in descs)
+    stream = torch.cuda.Stream(device=dev)
+    gather_bufs = None
+    if world > 1 and not args.no_gather:
+        n0 = max_local
+        if rank == 0:
+            gather_bufs = [[torch.empty(n0 * 6, dtype=torch.int32, device=dev) for _ in range(world)] for _ in range(nframes)]
+
+    def one_step(events=None):
+        with torch.cuda.stream(stream):
+            for f in range(nframes):
+                if events is not None:
+                    events[f][0].record(stream)
+                tree.cast(descs[f], outs[f], stream)
+                if events is not None:
+                    events[f][1].record(stream)
+            if world > 1 and not args.no_gather:
+                for f in range(nframes):
+                    o = outs[f]
+                    flat = torch.cat([o["pos_steps"].view(-1), o["t"].view(torch.int32), o["info"]])
+                    dist.gather(flat, gather_bufs[f] if rank == 0 else None, dst=0)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nframes)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [e[0].elapsed_time(e[1]) for step in evs for e in step]
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_rays = W * H * nframes * args.steps  # every rank's share of every frame, all steps
+    value = total_rays / elapsed
+    avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    rays_per_launch = rt.Tree.count(descs[0])
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    e_child, bray_meta = load_bray()
+    roof = None
+    if e_child is not None:
+        b_ray = 16.0 * (e_child + 1.0) + 4.0 * e_child + B_OUT
+        achieved = b_ray * rays_per_launch / avg_kernel_s / 1e9
+        traffic, _ = load_traffic()
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "bytes_per_ray": round(b_ray, 2), "avg_launch_ms": round(avg_kernel_s * 1e3, 4)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        hits = rt.decode_hits(outs[0])
+        cpu = cpu_baseline(ppx, ppy, hits)
+    line = {
+        "metric": "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols),
+        "config": {"workload": "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080 primary rays per GPU per "
+                               "step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % (args.cols, STEPS),
+                   "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
+                   "gather": world > 1 and not args.no_gather, "tree_nodes": info.n_nodes,
+                   "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 2)},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+/*
+ * svo_rt.h — C ABI of the MI355X-native sparse-voxel-tree primary raycaster (libsvo_rt.so).
+ *
+ * Drop-in boundary for reedthorngag/raytracing_test's hot path (paths relative to the reference):
+ *   - src/ray_caster.hpp:6-14          RayResult / RAY_CASTER::castRayFromCam(int steps)
+ *   - src/voxel_data/tetrahexa_tree.hpp:12-22  initTetraHexaTree / putBlock / getBlock / deleteBlock
+ *   - src/world_gen.hpp:3              genWorld()
+ *   - src/voxel_data/voxel_allocator.hpp:38-91  updateSsboData / initVoxelDataAllocator (device upload)
+ *   - src/shaders/low_res.frag:256-333,446-531  the per-pixel DDA + tree traversal, replaced by
+ *                                      svo_cast_rays() (a hand-written gfx950 HIP kernel)
+ *
+ * Conventions: every function returns an int status (SVO_OK = 0, negative on error) and never
+ * exits; svo_last_error() gives the message of the calling thread's last failure.  Pointers marked
+ * "device" are HBM pointers on the tree's device (e.g. a torch tensor's data_ptr()); a hip_stream
+ * argument is a hipStream_t (NULL = the null stream).  The tree is read-only during a cast.
+ */
+#ifndef SVO_RT_H
+#define SVO_RT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVO_RT_VERSION 1
+
+enum {
+    SVO_OK = 0,
+    SVO_EINVAL = -1,  /* bad argument */
+    SVO_ENOMEM = -2,  /* host or device allocation failed */
+    SVO_EDEVICE = -3, /* HIP runtime error / no GPU */
+    SVO_ESTATE = -4,  /* object not in the required state (e.g. tree not uploaded) */
+    SVO_ERANGE = -5   /* value outside what the structure supports */
+};
+
+/* Block (src/globals.hpp:76-80): leaf flags (bit 0 set for a stored voxel; REFLECTIVE 0x2,
+   REFRACTIVE 0x4, LUMINESCENT 0x8, LIQUID 0x10), 3 x 21-bit packed colour (src/types.hpp:6-9),
+   metadata.  The empty block is {0, ~0ull, 0}. */
+typedef struct {
+    uint32_t flags;
+    uint64_t color;
+    float metadata;
+} svo_block;
+
+/* RayResult (src/ray_caster.hpp:6-10) */
+typedef struct {
+    int32_t pos[3];
+    int32_t last_pos[3];
+    int32_t steps;
+} svo_ray_result;
+
+typedef struct svo_world svo_world; /* host-side editable 64-ary voxel tree */
+typedef struct svo_tree svo_tree;   /* breadth-first linearised tree (host image + HBM copy) */
+
+const char* svo_last_error(void);
+int svo_version(void);
+
+/* ---------------------------------------------------------------- world (host, editable) ---- */
+/* levels = descending tree levels; extent = 4^levels voxels per axis (reference: 5 -> 1024^3,
+   maxDepth 6 at src/voxel_data/tetrahexa_tree.hpp:6).  1 <= levels <= 7. */
+int svo_world_create(int32_t levels, svo_world** out);
+void svo_world_destroy(svo_world* w);
+/* initTetraHexaTree (tetrahexa_tree.cpp:13-41): root + the reference's 8 debug blocks.  The
+   reference's aliased root child array is NOT reproduced: the block at
+   (1000,1000,1000) exists here, while the reference cannot reach it. */
+int svo_init_tetra_hexa_tree(svo_world* w);
+/* putBlock (tetrahexa_tree.cpp:176-291): level levels+1 = one voxel (reference: 6), levels = a
+   4^3 block (reference: 5), ... 1 = the whole world.  Stored flags = 1 | b.flags. */
+int svo_put_block(svo_world* w, int32_t x, int32_t y, int32_t z, const svo_block* b, int32_t level);
+/* getBlock (tetrahexa_tree.cpp:113-157); coordinates wrap modulo the extent */
+int svo_get_block(const svo_world* w, int32_t x, int32_t y, int32_t z, svo_block* out);
+/* deleteBlock (tetrahexa_tree.cpp:293-359) with its intended meaning: clears the level-`level`
+   region containing (x,y,z) (level as putBlock's) and returns the block found there. */
+int svo_delete_block(svo_world* w, int32_t x, int32_t y, int32_t z, int32_t level, svo_block* removed);
+/* genWorld (world_gen.cpp:13-42) over width x length columns (reference: 200 x 200) */
+int svo_gen_world(svo_world* w, int32_t width, int32_t length);
+/* number of putBlock-visible tree nodes (diagnostics) */
+int svo_world_node_count(const svo_world* w, uint64_t* nodes);
+/* batched getBlock over n positions (xyz = 3 x int32 each) — the traverseTree batch lookup of
+   tetrahexa_tree.cpp:43-111, made usable */
+int svo_get_blocks(const svo_world* w, const int32_t* xyz, int64_t n, svo_block* out);
+/* batched putBlock of n blocks, all at `level`, applied in order */
+int svo_put_blocks(svo_world* w, const int32_t* xyz, const svo_block* blocks, int64_t n, int32_t level);
+/* OpenSimplex 2D (include/OpenSimplexNoise.cpp:77-208) for n points, and genWorld's column tops
+   (world_gen.cpp:22) for x in [0,width), z in [0,length): out[x*length + z] */
+int svo_noise2(int64_t seed, const double* x, const double* y, int64_t n, double* out);
+int svo_terrain_heights(int32_t width, int32_t length, int32_t nthreads, int32_t* out);
+
+/* ------------------------------------------------------------ tree (BFS, HBM-resident) ------ */
+typedef struct {
+    int32_t levels;
+    uint32_t n_materials;         /* palette entries including id 0 (empty) */
+    uint64_t n_nodes;             /* 16 B nodes */
+    uint64_t n_mat_bytes;         /* per-voxel material bytes of mixed-material bricks */
+    uint64_t n_bricks;            /* 4^3 brick nodes */
+    uint64_t nodes_per_level[8];  /* nodes at depth 0..levels-1 */
+    uint64_t device_bytes;        /* HBM footprint after svo_upload (0 before) */
+    int32_t device;               /* -1 before svo_upload */
+} svo_tree_info;
+
+/* Linearise a world: collapse uniform regions, drop non-solid (empty / LIQUID) voxels, emit the
+   breadth-first node array + material bytes + palette. */
+int svo_build(const svo_world* w, svo_tree** out);
+/* Build the same tree straight from genWorld's column formula over width x length columns
+   (no per-voxel putBlock: depth-12 / depth-14 terrain); nthreads host threads (0 = all). */
+int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out);
+int svo_tree_get_info(const svo_tree* t, svo_tree_info* out);
+/* palette entry `id` (id 0 = empty block) */
+int svo_tree_palette(const svo_tree* t, uint32_t id, svo_block* out);
+/* host-side lookup in the linearised tree; returns the solid-view block (empty for LIQUID) */
+int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32_t z, svo_block* out, uint32_t* material_id);
+/* batched host lookup: palette ids (0 = empty) of n positions */
+int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_t n, uint32_t* material_ids);
+/* copy the host image out (for tests / serialisation); byte sizes from svo_tree_get_info */
+int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nodes_bytes, void* mats, uint64_t mats_bytes);
+/* updateSsboData analogue: (re)upload the image to HBM of `device` */
+int svo_upload(svo_tree* t, int32_t device);
+void svo_tree_destroy(svo_tree* t);
+
+/* ---------------------------------------------------------------------------- casting ------- */
+/* Hit record per ray (caller-owned device buffers, 24 B / ray):
+     pos_steps[4*i .. 4*i+3] = {x, y, z, stepsLeft}   (RayResult.pos / .steps)
+     t[i]                    = deltaPos[axis] before its last increment (entry distance of pos)
+     info[i]                 = bit 31 hit | bits 16-17 last axis (3 = no step) | bit 18 step < 0
+                               on that axis | bits 0-15 material id (0 = none)
+   RayResult.lastPos = pos - (axis step).  Frame rays: index = row * width + px, rows counted
+   from the bottom (gl_FragCoord), restricted to the tile rows of this shard. */
+typedef struct {
+    int32_t* pos_steps;
+    float* t;
+    uint32_t* info;
+} svo_hits;
+
+typedef struct {
+    /* frame mode (ray_dirs == NULL): one primary ray per pixel, low_res.frag:264-288 */
+    float origin[3];   /* cameraPos (also the origin of explicit rays when ray_origins == NULL) */
+    float cam_dir[3];  /* normalised cameraDir */
+    int32_t width, height;
+    float ppx, ppy;    /* projPlaneSize uniform (main.cpp:94); see svo_proj_plane */
+    int32_t tile_row_start, tile_row_step; /* shard: 8-pixel tile rows start, start+step, ... */
+    /* explicit mode: n_rays rays, device float3 arrays */
+    const float* ray_dirs;
+    const float* ray_origins; /* optional */
+    int32_t n_rays;
+    int32_t steps;     /* DDA step budget per ray (castRayFromCam's `steps`) */
+    int32_t flags;     /* reserved, 0 */
+} svo_cast_desc;
+
+/* number of rays a desc produces on this shard (= records written) */
+int svo_cast_count(const svo_cast_desc* d, int64_t* n);
+/* asynchronous on hip_stream */
+int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* out, void* hip_stream);
+/* RAY_CASTER::castRayFromCam with explicit camera (synchronous, one ray on the GPU) */
+int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* out,
+                          svo_block* block);
+int svo_sync(void* hip_stream);
+
+/* host helpers shared bit-for-bit with the device code */
+int svo_proj_plane(int32_t width, int32_t height, float* ppx, float* ppy);
+int svo_normalize(const float v[3], float out[3]);
+int svo_pixel_dir(const float cam_dir[3], float ppx, float ppy, int32_t width, int32_t height, int32_t px, int32_t py,
+                  float out[3]);
+/* every pixel's direction, out[3 * (py * width + px) + a] */
+int svo_pixel_dirs(const float cam_dir[3], float ppx, float ppy, int32_t width, int32_t height, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVO_RT_H */

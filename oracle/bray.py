@@ -1,0 +1,38 @@
+"""ORACLE tool (test infrastructure): freeze SURVEY.md §8(d)'s algorithmic bytes per primary ray,
+B_ray = 16*E_node + 4*E_child + B_out with E_node = E_child + 1, where E_child counts node entries
+along the reference DDA path under the shader's common-ancestor restart (low_res.frag:493-531) on
+the reference-format tree.  Writes profiles/bray.json, which bench.py reads (it never imports the
+oracle for this).  Usage: python oracle/bray.py
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+B_OUT = 24
+
+
+def main():
+    res = {"formula": "B_ray = 16*(E_child+1) + 4*E_child + B_out, B_out = %d (this build's hit record)" % B_OUT,
+           "source": "oracle/bray.py (orc_frame_entries, oracle/oracle.c)"}
+    ref = O.Tree.reference_world()
+    for name, org, d, s in (("C2_cam0_S300", (35, 50, 35), (1, 0, 1), 300), ("C2_cam1_S300", (4, 90, 4), (1, -0.45, 1), 300),
+                            ("C2_cam1_S600", (4, 90, 4), (1, -0.45, 1), 600)):
+        e = ref.frame_entries(org, O.normalize(d), 1920, 1080, s, nthreads=8) / (1920 * 1080)
+        res[name] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT, "tree": "reference world (putBlock)"}
+    t = O.Tree.terrain(6, 4096, 4096)
+    e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, nthreads=8) / (1920 * 1080)
+    res["C3"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
+                 "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    json.dump(res, open(os.path.join(ROOT, "profiles", "bray.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,432 @@
+"""raytracing_test_amd — MI355X-native sparse-voxel-tree primary raycaster.
+
+Python host mirror of the C ABI in include/svo_rt.h (libsvo_rt.so, built in-tree by
+raytracing_test_amd/build.py).  Names follow the reference (reedthorngag/raytracing_test):
+
+    World.init_tetra_hexa_tree()   initTetraHexaTree()        src/voxel_data/tetrahexa_tree.cpp:13
+    World.put_block(...)           putBlock(Pos, Block, int)   src/voxel_data/tetrahexa_tree.cpp:176
+    World.get_block(...)           getBlock(Pos)               src/voxel_data/tetrahexa_tree.cpp:113
+    World.delete_block(...)        deleteBlock(Pos, int)       src/voxel_data/tetrahexa_tree.cpp:293
+    World.gen_world(w, l)          genWorld()                  src/world_gen.cpp:13
+    Tree.upload(device)            updateSsboData()            src/voxel_data/voxel_allocator.hpp:38
+    Tree.cast_ray_from_cam(...)    RAY_CASTER::castRayFromCam  src/ray_caster.cpp:54
+    Tree.cast_frame(...)           the low_res.frag per-pixel traversal, as one HIP launch
+
+There is no CPU fallback: every cast runs the gfx950 kernel, and importing this package without
+the built library raises.  torch is used only for device buffers and streams.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsvo_rt.so")
+
+SVO_OK = 0
+HIT_BIT = 1 << 31
+AXIS_SHIFT = 16
+NEG_BIT = 1 << 18
+MAT_MASK = 0xFFFF
+
+# Block flags (src/globals.hpp:68-74)
+NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
+
+
+class SvoError(RuntimeError):
+    pass
+
+
+class Block(C.Structure):
+    """Block (src/globals.hpp:76-80)."""
+
+    _fields_ = [("flags", C.c_uint32), ("color", C.c_uint64), ("metadata", C.c_float)]
+
+    def astuple(self):
+        return (self.flags, self.color, self.metadata)
+
+    def __repr__(self):
+        return "Block(flags=%#x, color=%#x, metadata=%g)" % self.astuple()
+
+
+class RayResult(C.Structure):
+    """RayResult (src/ray_caster.hpp:6-10)."""
+
+    _fields_ = [("pos", C.c_int32 * 3), ("last_pos", C.c_int32 * 3), ("steps", C.c_int32)]
+
+
+class TreeInfo(C.Structure):
+    _fields_ = [
+        ("levels", C.c_int32),
+        ("n_materials", C.c_uint32),
+        ("n_nodes", C.c_uint64),
+        ("n_mat_bytes", C.c_uint64),
+        ("n_bricks", C.c_uint64),
+        ("nodes_per_level", C.c_uint64 * 8),
+        ("device_bytes", C.c_uint64),
+        ("device", C.c_int32),
+    ]
+
+
+class CastDesc(C.Structure):
+    _fields_ = [
+        ("origin", C.c_float * 3),
+        ("cam_dir", C.c_float * 3),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("ppx", C.c_float),
+        ("ppy", C.c_float),
+        ("tile_row_start", C.c_int32),
+        ("tile_row_step", C.c_int32),
+        ("ray_dirs", C.c_void_p),
+        ("ray_origins", C.c_void_p),
+        ("n_rays", C.c_int32),
+        ("steps", C.c_int32),
+        ("flags", C.c_int32),
+    ]
+
+
+class Hits(C.Structure):
+    _fields_ = [("pos_steps", C.c_void_p), ("t", C.c_void_p), ("info", C.c_void_p)]
+
+
+_lib = None
+
+# every symbol include/svo_rt.h declares (tests check the library exports all of them)
+ABI_SYMBOLS = (
+    "svo_last_error", "svo_version", "svo_world_create", "svo_world_destroy", "svo_init_tetra_hexa_tree",
+    "svo_put_block", "svo_get_block", "svo_delete_block", "svo_gen_world", "svo_world_node_count", "svo_build",
+    "svo_build_terrain", "svo_tree_get_info", "svo_tree_palette", "svo_tree_get_block", "svo_tree_export",
+    "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
+    "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
+    "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights",
+)
+
+
+def lib():
+    """Load libsvo_rt.so (raises if it has not been built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libsvo_rt.so not built: run `python -m raytracing_test_amd.build` (or __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
+    f3 = C.POINTER(C.c_float)
+    L.svo_last_error.restype = C.c_char_p
+    L.svo_world_create.argtypes = [i32, C.POINTER(vp)]
+    L.svo_world_destroy.argtypes = [vp]
+    L.svo_world_destroy.restype = None
+    L.svo_init_tetra_hexa_tree.argtypes = [vp]
+    L.svo_put_block.argtypes = [vp, i32, i32, i32, C.POINTER(Block), i32]
+    L.svo_get_block.argtypes = [vp, i32, i32, i32, C.POINTER(Block)]
+    L.svo_delete_block.argtypes = [vp, i32, i32, i32, i32, C.POINTER(Block)]
+    L.svo_gen_world.argtypes = [vp, i32, i32]
+    L.svo_world_node_count.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.svo_build.argtypes = [vp, C.POINTER(vp)]
+    L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
+    L.svo_tree_get_info.argtypes = [vp, C.POINTER(TreeInfo)]
+    L.svo_tree_palette.argtypes = [vp, C.c_uint32, C.POINTER(Block)]
+    L.svo_tree_get_block.argtypes = [vp, i32, i32, i32, C.POINTER(Block), C.POINTER(C.c_uint32)]
+    L.svo_tree_export.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64]
+    L.svo_upload.argtypes = [vp, i32]
+    L.svo_tree_destroy.argtypes = [vp]
+    L.svo_tree_destroy.restype = None
+    L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
+    L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
+    L.svo_cast_ray_from_cam.argtypes = [vp, f3, f3, i32, C.POINTER(RayResult), C.POINTER(Block)]
+    L.svo_sync.argtypes = [vp]
+    L.svo_proj_plane.argtypes = [i32, i32, C.POINTER(f32), C.POINTER(f32)]
+    L.svo_normalize.argtypes = [f3, f3]
+    L.svo_pixel_dir.argtypes = [f3, f32, f32, i32, i32, i32, i32, f3]
+    L.svo_pixel_dirs.argtypes = [f3, f32, f32, i32, i32, vp]
+    L.svo_get_blocks.argtypes = [vp, vp, C.c_int64, vp]
+    L.svo_put_blocks.argtypes = [vp, vp, vp, C.c_int64, i32]
+    L.svo_tree_get_blocks.argtypes = [vp, vp, C.c_int64, vp]
+    L.svo_noise2.argtypes = [C.c_int64, vp, vp, C.c_int64, vp]
+    L.svo_terrain_heights.argtypes = [i32, i32, i32, vp]
+    _lib = L
+    return L
+
+
+def _check(rc, what):
+    if rc != SVO_OK:
+        msg = lib().svo_last_error()
+        raise SvoError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def _f3(v):
+    a = (C.c_float * 3)(*[float(x) for x in v])
+    return a
+
+
+def proj_plane(width, height):
+    """projPlaneSize uniform of src/main.cpp:94."""
+    a, b = C.c_float(), C.c_float()
+    _check(lib().svo_proj_plane(width, height, C.byref(a), C.byref(b)), "svo_proj_plane")
+    return a.value, b.value
+
+
+def normalize(v):
+    """glm::normalize in float (the camera direction of src/main.cpp:195)."""
+    o = (C.c_float * 3)()
+    _check(lib().svo_normalize(_f3(v), o), "svo_normalize")
+    return np.array(list(o), np.float32)
+
+
+def pixel_dir(cam_dir, ppx, ppy, width, height, px, py):
+    o = (C.c_float * 3)()
+    _check(lib().svo_pixel_dir(_f3(cam_dir), ppx, ppy, width, height, px, py, o), "svo_pixel_dir")
+    return np.array(list(o), np.float32)
+
+
+def pixel_dirs(cam_dir, width, height, ppx=None, ppy=None):
+    """Every pixel's primary-ray direction, shape (height, width, 3), rows from the bottom."""
+    if ppx is None:
+        ppx, ppy = proj_plane(width, height)
+    out = np.zeros((height, width, 3), np.float32)
+    _check(lib().svo_pixel_dirs(_f3(cam_dir), ppx, ppy, width, height, out.ctypes.data_as(C.c_void_p)), "svo_pixel_dirs")
+    return out
+
+
+def noise2(seed, x, y):
+    """OpenSimplex 2D (include/OpenSimplexNoise.cpp:77-208) at arrays of points."""
+    x = np.ascontiguousarray(x, np.float64)
+    y = np.ascontiguousarray(y, np.float64)
+    out = np.zeros(len(x), np.float64)
+    _check(lib().svo_noise2(int(seed), x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p), len(x),
+                            out.ctypes.data_as(C.c_void_p)), "svo_noise2")
+    return out
+
+
+def terrain_heights(width, length, nthreads=0):
+    """genWorld's column tops (world_gen.cpp:22), shape (width, length)."""
+    out = np.zeros((width, length), np.int32)
+    _check(lib().svo_terrain_heights(width, length, nthreads, out.ctypes.data_as(C.c_void_p)), "svo_terrain_heights")
+    return out
+
+
+def _xyz(points):
+    return np.ascontiguousarray(np.asarray(points, dtype=np.int32).reshape(-1, 3))
+
+
+class World:
+    """Host-side editable 64-ary voxel tree (the reference's global `root` + pools)."""
+
+    def __init__(self, levels=5):
+        self.levels = levels
+        h = C.c_void_p()
+        _check(lib().svo_world_create(levels, C.byref(h)), "svo_world_create")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.svo_world_destroy(self._h)
+            self._h = None
+
+    @classmethod
+    def reference(cls, width=200, length=200):
+        """initTetraHexaTree() + genWorld(): the reference application's world (1024^3)."""
+        w = cls(5)
+        w.init_tetra_hexa_tree()
+        w.gen_world(width, length)
+        return w
+
+    def init_tetra_hexa_tree(self):
+        _check(lib().svo_init_tetra_hexa_tree(self._h), "svo_init_tetra_hexa_tree")
+
+    def put_block(self, x, y, z, flags, color, metadata=0.0, level=None):
+        b = Block(flags, color, metadata)
+        lv = self.levels + 1 if level is None else level
+        _check(lib().svo_put_block(self._h, x, y, z, C.byref(b), lv), "svo_put_block")
+
+    def get_block(self, x, y, z):
+        b = Block()
+        _check(lib().svo_get_block(self._h, x, y, z, C.byref(b)), "svo_get_block")
+        return b.astuple()
+
+    def delete_block(self, x, y, z, level=None):
+        b = Block()
+        lv = self.levels + 1 if level is None else level
+        _check(lib().svo_delete_block(self._h, x, y, z, lv, C.byref(b)), "svo_delete_block")
+        return b.astuple()
+
+    def get_blocks(self, points):
+        """Batched getBlock: returns (flags u32, color u64, metadata f32) arrays."""
+        p = _xyz(points)
+        out = (Block * len(p))()
+        _check(lib().svo_get_blocks(self._h, p.ctypes.data_as(C.c_void_p), len(p), C.cast(out, C.c_void_p)), "svo_get_blocks")
+        a = np.frombuffer(out, dtype=np.dtype([("flags", "<u4"), ("pad", "<u4"), ("color", "<u8"), ("metadata", "<f4"), ("pad2", "<u4")]))
+        return a["flags"].copy(), a["color"].copy(), a["metadata"].copy()
+
+    def put_blocks(self, points, flags, colors, metadata=None, level=None):
+        p = _xyz(points)
+        n = len(p)
+        arr = (Block * n)()
+        a = np.frombuffer(arr, dtype=np.dtype([("flags", "<u4"), ("pad", "<u4"), ("color", "<u8"), ("metadata", "<f4"), ("pad2", "<u4")]))
+        a["flags"] = flags
+        a["color"] = colors
+        a["metadata"] = 0.0 if metadata is None else metadata
+        lv = self.levels + 1 if level is None else level
+        _check(lib().svo_put_blocks(self._h, p.ctypes.data_as(C.c_void_p), C.cast(arr, C.c_void_p), n, lv), "svo_put_blocks")
+
+    def gen_world(self, width=200, length=200):
+        _check(lib().svo_gen_world(self._h, width, length), "svo_gen_world")
+
+    def node_count(self):
+        n = C.c_uint64()
+        _check(lib().svo_world_node_count(self._h, C.byref(n)), "svo_world_node_count")
+        return n.value
+
+    def build(self):
+        h = C.c_void_p()
+        _check(lib().svo_build(self._h, C.byref(h)), "svo_build")
+        return Tree(h)
+
+
+def _torch():
+    import torch  # plumbing only: device buffers and streams
+
+    return torch
+
+
+class Tree:
+    """Breadth-first linearised tree: host image + HBM copy after upload()."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self._scratch = {}
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.svo_tree_destroy(self._h)
+            self._h = None
+
+    @classmethod
+    def terrain(cls, levels, width, length, nthreads=0):
+        """genWorld's column formula over width x length columns, built without per-voxel putBlock."""
+        h = C.c_void_p()
+        _check(lib().svo_build_terrain(levels, width, length, nthreads, C.byref(h)), "svo_build_terrain")
+        return cls(h)
+
+    def info(self):
+        i = TreeInfo()
+        _check(lib().svo_tree_get_info(self._h, C.byref(i)), "svo_tree_get_info")
+        return i
+
+    def palette(self):
+        out = []
+        for k in range(self.info().n_materials):
+            b = Block()
+            _check(lib().svo_tree_palette(self._h, k, C.byref(b)), "svo_tree_palette")
+            out.append(b.astuple())
+        return out
+
+    def get_block(self, x, y, z):
+        b, m = Block(), C.c_uint32()
+        _check(lib().svo_tree_get_block(self._h, x, y, z, C.byref(b), C.byref(m)), "svo_tree_get_block")
+        return b.astuple(), m.value
+
+    def get_blocks(self, points):
+        """Batched lookup in the linearised tree: palette ids (0 = empty, LIQUID counts as empty)."""
+        p = _xyz(points)
+        ids = np.zeros(len(p), np.uint32)
+        _check(lib().svo_tree_get_blocks(self._h, p.ctypes.data_as(C.c_void_p), len(p), ids.ctypes.data_as(C.c_void_p)),
+               "svo_tree_get_blocks")
+        return ids
+
+    def export(self):
+        i = self.info()
+        nodes = np.zeros(i.n_nodes * 2, np.uint64)
+        mats = np.zeros(max(1, i.n_mat_bytes // 2), np.uint16)
+        _check(lib().svo_tree_export(self._h, nodes.ctypes.data_as(C.c_void_p), nodes.nbytes,
+                                     mats.ctypes.data_as(C.c_void_p), mats.nbytes), "svo_tree_export")
+        return nodes.reshape(-1, 2), mats[: i.n_mat_bytes // 2]
+
+    def upload(self, device=0):
+        _check(lib().svo_upload(self._h, device), "svo_upload")
+        return self
+
+    # ------------------------------------------------------------------------------ casting --
+    @staticmethod
+    def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1):
+        if ppx is None:
+            ppx, ppy = proj_plane(width, height)
+        d = CastDesc()
+        d.origin[:] = [float(x) for x in origin]
+        d.cam_dir[:] = [float(x) for x in cam_dir]
+        d.width, d.height, d.ppx, d.ppy = width, height, ppx, ppy
+        d.tile_row_start, d.tile_row_step = tile_row_start, tile_row_step
+        d.steps = steps
+        return d
+
+    @staticmethod
+    def count(desc):
+        n = C.c_int64()
+        _check(lib().svo_cast_count(C.byref(desc), C.byref(n)), "svo_cast_count")
+        return n.value
+
+    @staticmethod
+    def alloc_hits(n, device):
+        torch = _torch()
+        dev = torch.device("cuda", device)
+        return dict(
+            pos_steps=torch.empty((n, 4), dtype=torch.int32, device=dev),
+            t=torch.empty(n, dtype=torch.float32, device=dev),
+            info=torch.empty(n, dtype=torch.int32, device=dev),
+        )
+
+    def cast(self, desc, out, stream=None):
+        """Launch the cast kernel asynchronously on `stream` (a torch.cuda.Stream or raw handle)."""
+        h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr())
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_cast_rays(self._h, C.byref(desc), C.byref(h), C.c_void_p(s) if s else None), "svo_cast_rays")
+
+    def cast_frame(self, origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1,
+                   out=None, stream=None, sync=True):
+        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step)
+        n = self.count(d)
+        if out is None:
+            out = self.alloc_hits(n, self.info().device)
+        self.cast(d, out, stream)
+        if sync:
+            _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
+        return out
+
+    def cast_rays(self, dirs, origins=None, steps=300, origin=(0.0, 0.0, 0.0), out=None, stream=None, sync=True):
+        """Explicit rays: dirs / origins are (n, 3) float32 device tensors."""
+        d = CastDesc()
+        d.origin[:] = [float(x) for x in origin]
+        d.ray_dirs = dirs.data_ptr()
+        d.ray_origins = origins.data_ptr() if origins is not None else None
+        d.n_rays = dirs.shape[0]
+        d.steps = steps
+        if out is None:
+            out = self.alloc_hits(d.n_rays, self.info().device)
+        self.cast(d, out, stream)
+        if sync:
+            _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
+        return out
+
+    def cast_ray_from_cam(self, pos, cam_dir, steps):
+        """RAY_CASTER::castRayFromCam(steps) with the camera passed in: (RayResult, Block)."""
+        r, b = RayResult(), Block()
+        _check(lib().svo_cast_ray_from_cam(self._h, _f3(pos), _f3(cam_dir), steps, C.byref(r), C.byref(b)),
+               "svo_cast_ray_from_cam")
+        return (tuple(r.pos), tuple(r.last_pos), r.steps), b.astuple()
+
+
+def decode_hits(out):
+    """Device hit buffers -> numpy dict (pos, last_pos, steps, hit, axis, material, t)."""
+    ps = out["pos_steps"].cpu().numpy()
+    info = out["info"].cpu().numpy().view(np.uint32)
+    t = out["t"].cpu().numpy()
+    axis = (info >> AXIS_SHIFT) & 3
+    neg = (info & NEG_BIT) != 0
+    pos = ps[:, :3].copy()
+    last = pos.copy()
+    for a in range(3):
+        sel = axis == a
+        last[sel, a] -= np.where(neg[sel], -1, 1)
+    return dict(pos=pos, last_pos=last, steps=ps[:, 3].copy(), hit=(info & HIT_BIT) != 0, axis=axis.astype(np.int32),
+                material=(info & MAT_MASK).astype(np.int32), t=t)

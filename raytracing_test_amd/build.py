@@ -1,0 +1,59 @@
+"""Build libsvo_rt.so in-tree for gfx950 (hipcc for the kernels, g++ for the host builder).
+
+Flags that matter for parity: -ffp-contract=off everywhere (no FMA contraction of the FP64 DDA,
+the noise or the float ray generation), no fast-math.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "libsvo_rt.so")
+BUILD = os.path.join(HERE, "_build")
+ARCH = os.environ.get("SVO_OFFLOAD_ARCH", "gfx950")
+
+HOST_SRCS = ["svo_world.cpp"]
+HIP_SRCS = ["svo_cast.hip"]
+HEADERS = ["svo_common.h", "svo_noise.h", "svo_internal.h"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+
+
+def build(force=False, verbose=False):
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    os.makedirs(BUILD, exist_ok=True)
+    hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "svo_rt.h")]
+    objs = []
+    for s in HOST_SRCS:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-Wall",
+                  "-c", src, "-o", obj])
+        objs.append(obj)
+    for s in HIP_SRCS:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run([hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+                  "-Wall", "-c", src, "-o", obj])
+        objs.append(obj)
+    if force or _newer(OUT, objs):
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT] + objs + ["-pthread"])
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

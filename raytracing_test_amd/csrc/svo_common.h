@@ -1,0 +1,138 @@
+// svo_common.h — definitions shared by the host builder (svo_world.cpp) and the gfx950 kernels
+// (svo_cast.hip).  Everything arithmetic here is compiled with -ffp-contract=off on both sides and
+// rounds identically on x86-64 and gfx950: float divisions and square roots go through double
+// precision and are rounded once to float (double rounding is innocuous for +,-,*,/,sqrt when the
+// wide format has >= 2p+2 bits: 53 >= 50), so no result depends on a compiler's fp32 div/sqrt mode.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SVO_HD __host__ __device__ __forceinline__
+#else
+#define SVO_HD static inline
+#endif
+
+namespace svo {
+
+// ------------------------------------------------------------------------------------------------
+// Linearised tree node, 16 B (the reference's node is 16 B too: src/voxel_data/types.hpp:29-47, but
+// its children live in 256 B pointer arrays; here children are contiguous in breadth-first order
+// and addressed by popcount of a 64-bit child mask — the variant the reference sketches at
+// tetrahexa_tree.cpp:144-145).
+//   kind INTERIOR: mask bit i = child i (index z<<4 | y<<2 | x) holds a solid voxel;
+//                  ref = node index of the first child; child i = ref + popcount(mask & (2^i - 1))
+//   kind BRICK   : a 4^3 region at depth levels-1; mask bit v = voxel v is solid;
+//                  info & UNIFORM -> every solid voxel has material info>>16,
+//                  else material of voxel v = mats[ref + popcount(mask & (2^v - 1))]
+//   kind SOLID   : the whole region is solid with material info>>16 (mask = ~0)
+// The root is node 0; an empty world is an INTERIOR root with mask 0.
+// ------------------------------------------------------------------------------------------------
+struct alignas(16) Node {
+    uint64_t mask;
+    uint32_t ref;
+    uint32_t info;
+};
+static_assert(sizeof(Node) == 16, "node must be 16 B");
+
+enum : uint32_t { K_INTERIOR = 0u, K_BRICK = 1u, K_SOLID = 2u, K_KIND_MASK = 3u, K_UNIFORM = 4u };
+
+SVO_HD uint32_t node_kind(uint32_t info) { return info & K_KIND_MASK; }
+SVO_HD uint32_t node_material(uint32_t info) { return info >> 16; }
+
+// child slot of wrapped voxel coordinates at bit offset `sh` (tetrahexa_tree.cpp:127-129)
+SVO_HD uint32_t child_slot(uint32_t x, uint32_t y, uint32_t z, uint32_t sh) {
+    return (((z >> sh) & 3u) << 4) | (((y >> sh) & 3u) << 2) | ((x >> sh) & 3u);
+}
+
+// hit-record info word (see include/svo_rt.h)
+enum : uint32_t { HIT_BIT = 1u << 31, AXIS_SHIFT = 16, NEG_BIT = 1u << 18, MAT_MASK = 0xFFFFu };
+
+// ------------------------------------------------------------------------------------------------
+// Correctly rounded f32 division / sqrt via f64 (see header note)
+// ------------------------------------------------------------------------------------------------
+SVO_HD float div_rn(float a, float b) { return (float)((double)a / (double)b); }
+#if defined(__HIP_DEVICE_COMPILE__)
+SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
+#else
+SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
+#endif
+
+// glm::cross (x.y*y.z - y.y*x.z, x.z*y.x - y.z*x.x, x.x*y.y - y.x*x.y)
+SVO_HD void cross3(const float a[3], const float b[3], float o[3]) {
+    o[0] = a[1] * b[2] - b[1] * a[2];
+    o[1] = a[2] * b[0] - b[2] * a[0];
+    o[2] = a[0] * b[1] - b[0] * a[1];
+}
+
+// glm::normalize: v * (1 / sqrt((x*x + y*y) + z*z))
+SVO_HD void normalize3(const float v[3], float o[3]) {
+    float d = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
+    float r = div_rn(1.0f, sqrt_rn(d));
+    o[0] = v[0] * r;
+    o[1] = v[1] * r;
+    o[2] = v[2] * r;
+}
+
+// Per-pixel primary ray (src/shaders/low_res.frag:264-288): FragCoord = gl_FragCoord.xy * (1/res)
+// with the pixel centre at +0.5 and rows counted from the bottom; `left` is cross(dir, up)
+// unnormalised (the shader's projection_plane_left), `up' = cross(dir, left)`;
+// d = normalize((dir + left * -(ppx * (fx - 0.5))) + (up' * (-fy + 0.5)) * ppy).
+struct RayGen {
+    float c[3], l[3], u[3];
+    float ppx, ppy, rw, rh;
+};
+
+SVO_HD void raygen_init(RayGen& g, const float cam[3], float ppx, float ppy, int32_t w, int32_t h) {
+    const float up[3] = {0.0f, 1.0f, 0.0f};
+    g.c[0] = cam[0];
+    g.c[1] = cam[1];
+    g.c[2] = cam[2];
+    cross3(g.c, up, g.l);
+    cross3(g.c, g.l, g.u);
+    g.ppx = ppx;
+    g.ppy = ppy;
+    g.rw = div_rn(1.0f, (float)w);
+    g.rh = div_rn(1.0f, (float)h);
+}
+
+SVO_HD void raygen_pixel(const RayGen& g, int32_t px, int32_t py, float d[3]) {
+    float fx = ((float)px + 0.5f) * g.rw;
+    float fy = ((float)py + 0.5f) * g.rh;
+    float sl = -(g.ppx * (fx - 0.5f));
+    float su = -fy + 0.5f;
+    float v[3];
+    for (int a = 0; a < 3; a++) {
+        float lt = g.l[a] * sl;
+        float ut = (g.u[a] * su) * g.ppy;
+        v[a] = (g.c[a] + lt) + ut;
+    }
+    normalize3(v, d);
+}
+
+// ------------------------------------------------------------------------------------------------
+// DDA set-up of RAY_CASTER::buildRay + castRayFromCam (src/ray_caster.cpp:19-66): step = sign with
+// -0.0 / NaN -> +1; delta = 1/dir as a FLOAT division widened to double; absDelta = glm::abs;
+// round = trunc(origin); exact = origin - 1 on negative-step axes;
+// deltaPos = absDelta - (exact - round) * delta  (the product is exact in double).
+// ------------------------------------------------------------------------------------------------
+struct Dda1 {
+    int32_t step;
+    int32_t cell;
+    double adelta;
+    double dpos;
+};
+
+SVO_HD Dda1 dda_axis(float o, float d) {
+    Dda1 r;
+    r.step = d < 0.0f ? -1 : 1;
+    double delta = (double)div_rn(1.0f, d);
+    r.adelta = delta >= 0.0 ? delta : -delta;
+    r.cell = (int32_t)__builtin_truncf(o);
+    double exact = (double)o;
+    if (r.step < 0) exact -= 1.0;
+    r.dpos = r.adelta - (exact - (double)r.cell) * delta;
+    return r;
+}
+
+}  // namespace svo

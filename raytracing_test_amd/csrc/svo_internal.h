@@ -1,0 +1,58 @@
+// svo_internal.h — host-side object layouts shared by svo_world.cpp (builders, C++ host) and
+// svo_cast.hip (device upload + kernels).  Not part of the public ABI (include/svo_rt.h).
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "svo_common.h"
+
+namespace svo {
+
+struct Material {
+    uint32_t flags;
+    uint64_t color;
+    float meta;
+};
+
+inline bool material_solid(const Material& m) {
+    // castRayFromCam's hit test (ray_caster.cpp:82)
+    return m.color != ~0ull && (m.flags & 0x10u) == 0;
+}
+
+void set_error(const std::string& msg);
+
+// RGB_TO_U64 (src/types.hpp:6-9)
+inline uint64_t rgb_to_u64(int r, int g, int b) {
+    auto cs = [](int c) -> uint64_t {
+        return (uint64_t)((double)(float)c / 255.0 * (double)((1 << 21) - 1)) & ((1u << 21) - 1);
+    };
+    return (cs(r) << 42) | (cs(g) << 21) | cs(b);
+}
+
+}  // namespace svo
+
+// Linearised tree: host image + optional HBM copy
+struct svo_tree {
+    int32_t levels = 0;
+    std::vector<svo::Node> nodes;
+    std::vector<uint16_t> mats;           // per-voxel material ids of mixed-material bricks
+    std::vector<svo::Material> palette;   // id 0 = empty block {0, ~0, 0}
+    uint64_t nodes_per_level[8] = {0};
+    uint64_t n_bricks = 0;
+    // device side (svo_cast.hip)
+    int32_t device = -1;
+    void* d_nodes = nullptr;
+    void* d_mats = nullptr;
+    void* d_work = nullptr;   // scheduler counters (ring)
+    uint32_t work_slots = 0;
+    uint32_t work_next = 0;
+    uint64_t device_bytes = 0;
+    uint32_t lds_nodes = 0;   // top-of-tree nodes staged in LDS by the cast kernel
+};
+
+namespace svo {
+void tree_release_device(svo_tree* t);  // svo_cast.hip
+}

@@ -1,0 +1,871 @@
+// svo_world.cpp — host side of libsvo_rt: the editable 64-ary voxel world (the reference's
+// putBlock / getBlock / deleteBlock / genWorld API), and the two builders that emit the
+// breadth-first linearised tree the gfx950 kernel walks:
+//   * svo_build          — from an edited world (reference world: initTetraHexaTree + genWorld)
+//   * svo_build_terrain  — straight from genWorld's column formula, level-synchronous and
+//                          multi-threaded, for depth-12 / depth-14 terrain that the reference's
+//                          one-leaf-per-voxel layout cannot hold.
+// Both emit the same canonical form (tests check they agree node for node), defined in
+// svo_common.h.  Reference paths are relative to the reedthorngag/raytracing_test snapshot.
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <functional>
+#include <map>
+#include <thread>
+#include <vector>
+
+#include "../../include/svo_rt.h"
+#include "svo_internal.h"
+#include "svo_noise.h"
+
+using namespace svo;
+
+static thread_local std::string g_err;
+void svo::set_error(const std::string& msg) { g_err = msg; }
+
+extern "C" const char* svo_last_error(void) { return g_err.c_str(); }
+extern "C" int svo_version(void) { return SVO_RT_VERSION; }
+
+#define SVO_FAIL(code, msg)     \
+    do {                        \
+        svo::set_error(msg);    \
+        return (code);          \
+    } while (0)
+
+static void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn) {
+    if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+    nthreads = (int)std::min<int64_t>(nthreads, std::max<int64_t>(1, n / 64));
+    if (nthreads <= 1 || n < 2) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    std::atomic<int64_t> next(0);
+    const int64_t chunk = std::max<int64_t>(1, n / (nthreads * 8));
+    for (int i = 0; i < nthreads; i++)
+        th.emplace_back([&] {
+            for (;;) {
+                int64_t b = next.fetch_add(chunk);
+                if (b >= n) break;
+                fn(b, std::min(n, b + chunk));
+            }
+        });
+    for (auto& t : th) t.join();
+}
+
+// ================================================================================================
+// Palette
+// ================================================================================================
+namespace {
+struct Palette {
+    std::vector<Material> m;
+    std::map<std::tuple<uint32_t, uint64_t, uint32_t>, uint16_t> index;
+    Palette() { m.push_back(Material{0, ~0ull, 0.0f}); }
+    int intern(const Material& x) {
+        uint32_t mb;
+        memcpy(&mb, &x.meta, 4);
+        auto key = std::make_tuple(x.flags, x.color, mb);
+        auto it = index.find(key);
+        if (it != index.end()) return it->second;
+        if (m.size() >= 0xFFFFu) return -1;
+        uint16_t id = (uint16_t)m.size();
+        m.push_back(x);
+        index[key] = id;
+        return id;
+    }
+};
+}  // namespace
+
+// ================================================================================================
+// Editable world: a 64-ary pointer tree with the reference's semantics (tetrahexa_tree.cpp), minus
+// its root-array aliasing.  Node 0 is the root; a child id of 0 means "absent" (bitmap bit clear).
+// Leaves may sit at any depth (putBlock level < levels+1 stores a uniform region).
+// ================================================================================================
+struct svo_world {
+    int32_t levels;
+    Palette pal;
+    struct ENode {
+        uint32_t kids;  // branch: index of its 64-slot child block
+        uint16_t mat;   // leaf: palette id
+        uint8_t leaf;
+    };
+    std::vector<ENode> nodes;
+    std::vector<uint32_t> kid_blocks;  // 64 ids per block
+    std::vector<uint32_t> free_nodes, free_blocks;
+    uint64_t live_nodes = 0;
+
+    uint32_t new_block() {
+        uint32_t b;
+        if (!free_blocks.empty()) {
+            b = free_blocks.back();
+            free_blocks.pop_back();
+        } else {
+            b = (uint32_t)(kid_blocks.size() / 64);
+            kid_blocks.resize(kid_blocks.size() + 64);
+        }
+        std::fill(kid_blocks.begin() + (size_t)b * 64, kid_blocks.begin() + (size_t)b * 64 + 64, 0u);
+        return b;
+    }
+    uint32_t new_node(uint8_t leaf, uint16_t mat) {
+        uint32_t n;
+        if (!free_nodes.empty()) {
+            n = free_nodes.back();
+            free_nodes.pop_back();
+        } else {
+            n = (uint32_t)nodes.size();
+            nodes.push_back(ENode{0, 0, 0});
+        }
+        nodes[n].leaf = leaf;
+        nodes[n].mat = mat;
+        nodes[n].kids = leaf ? 0 : new_block();
+        live_nodes++;
+        return n;
+    }
+    uint32_t* kids(uint32_t n) { return &kid_blocks[(size_t)nodes[n].kids * 64]; }
+    const uint32_t* kids(uint32_t n) const { return &kid_blocks[(size_t)nodes[n].kids * 64]; }
+    // deleteChildren (tetrahexa_tree.cpp:159-173)
+    void drop_children(uint32_t n) {
+        if (nodes[n].leaf) return;
+        uint32_t b = nodes[n].kids;
+        for (int i = 0; i < 64; i++) {
+            uint32_t c = kid_blocks[(size_t)b * 64 + i];
+            if (c) {
+                drop_children(c);
+                free_nodes.push_back(c);
+                live_nodes--;
+            }
+        }
+        free_blocks.push_back(b);
+    }
+    void make_leaf(uint32_t n, uint16_t mat) {
+        drop_children(n);
+        nodes[n].leaf = 1;
+        nodes[n].mat = mat;
+        nodes[n].kids = 0;
+    }
+    // split a leaf into 64 copies of itself (tetrahexa_tree.cpp:221-247)
+    void split(uint32_t n) {
+        uint16_t m = nodes[n].mat;
+        uint32_t b = new_block();
+        for (int i = 0; i < 64; i++) {
+            uint32_t c = new_node(1, m);
+            kid_blocks[(size_t)b * 64 + i] = c;
+        }
+        nodes[n].leaf = 0;
+        nodes[n].kids = b;
+    }
+    uint32_t wrapmask() const { return (1u << (2 * levels)) - 1u; }
+};
+
+extern "C" int svo_world_create(int32_t levels, svo_world** out) {
+    if (!out) SVO_FAIL(SVO_EINVAL, "svo_world_create: out is NULL");
+    if (levels < 1 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_world_create: levels must be in [1, 7]");
+    svo_world* w = new (std::nothrow) svo_world();
+    if (!w) SVO_FAIL(SVO_ENOMEM, "svo_world_create: out of memory");
+    w->levels = levels;
+    w->new_node(0, 0);  // root: an empty branch (tetrahexa_tree.cpp:15-18)
+    *out = w;
+    return SVO_OK;
+}
+
+extern "C" void svo_world_destroy(svo_world* w) { delete w; }
+
+extern "C" int svo_world_node_count(const svo_world* w, uint64_t* n) {
+    if (!w || !n) SVO_FAIL(SVO_EINVAL, "svo_world_node_count: NULL argument");
+    *n = w->live_nodes;
+    return SVO_OK;
+}
+
+static int put_block_id(svo_world* w, int32_t x, int32_t y, int32_t z, uint16_t mat, int32_t level) {
+    const int target = level - 1;  // putBlock: `level--` (tetrahexa_tree.cpp:178)
+    const uint32_t mk = w->wrapmask();
+    const uint32_t wx = (uint32_t)x & mk, wy = (uint32_t)y & mk, wz = (uint32_t)z & mk;
+    uint32_t n = 0;
+    for (int depth = 0;; depth++) {
+        if (depth == target) {
+            w->make_leaf(n, mat);
+            return SVO_OK;
+        }
+        if (w->nodes[n].leaf) w->split(n);
+        const uint32_t slot = child_slot(wx, wy, wz, (uint32_t)(2 * (w->levels - 1 - depth)));
+        uint32_t c = w->kids(n)[slot];
+        if (!c) {
+            if (depth + 1 == target) {
+                c = w->new_node(1, mat);
+                w->kids(n)[slot] = c;
+                return SVO_OK;
+            }
+            c = w->new_node(0, 0);
+            w->kids(n)[slot] = c;
+        }
+        n = c;
+    }
+}
+
+extern "C" int svo_put_block(svo_world* w, int32_t x, int32_t y, int32_t z, const svo_block* b, int32_t level) {
+    if (!w || !b) SVO_FAIL(SVO_EINVAL, "svo_put_block: NULL argument");
+    if (level < 1 || level > w->levels + 1) SVO_FAIL(SVO_EINVAL, "svo_put_block: level out of range");
+    int id = w->pal.intern(Material{1u | b->flags, b->color, b->metadata});
+    if (id < 0) SVO_FAIL(SVO_ERANGE, "svo_put_block: more than 65534 distinct blocks");
+    return put_block_id(w, x, y, z, (uint16_t)id, level);
+}
+
+extern "C" int svo_get_block(const svo_world* w, int32_t x, int32_t y, int32_t z, svo_block* out) {
+    if (!w || !out) SVO_FAIL(SVO_EINVAL, "svo_get_block: NULL argument");
+    const uint32_t mk = w->wrapmask();
+    const uint32_t wx = (uint32_t)x & mk, wy = (uint32_t)y & mk, wz = (uint32_t)z & mk;
+    uint32_t n = 0;
+    for (int depth = 0; depth <= w->levels; depth++) {
+        if (w->nodes[n].leaf) {
+            const Material& m = w->pal.m[w->nodes[n].mat];
+            *out = svo_block{m.flags, m.color, m.meta};
+            return SVO_OK;
+        }
+        if (depth == w->levels) break;
+        uint32_t c = w->kids(n)[child_slot(wx, wy, wz, (uint32_t)(2 * (w->levels - 1 - depth)))];
+        if (!c) {
+            *out = svo_block{0, ~0ull, 0.0f};
+            return SVO_OK;
+        }
+        n = c;
+    }
+    SVO_FAIL(SVO_ESTATE, "svo_get_block: branch at voxel depth (corrupt world)");
+}
+
+extern "C" int svo_delete_block(svo_world* w, int32_t x, int32_t y, int32_t z, int32_t level, svo_block* removed) {
+    if (!w) SVO_FAIL(SVO_EINVAL, "svo_delete_block: NULL world");
+    if (level < 1 || level > w->levels + 1) SVO_FAIL(SVO_EINVAL, "svo_delete_block: level out of range");
+    const int target = level - 1;
+    const uint32_t mk = w->wrapmask();
+    const uint32_t wx = (uint32_t)x & mk, wy = (uint32_t)y & mk, wz = (uint32_t)z & mk;
+    svo_block found{0, ~0ull, 0.0f};
+    if (target == 0) {
+        if (w->nodes[0].leaf) {
+            const Material& m = w->pal.m[w->nodes[0].mat];
+            found = svo_block{m.flags, m.color, m.meta};
+        }
+        w->drop_children(0);
+        w->nodes[0].leaf = 0;
+        w->nodes[0].kids = w->new_block();
+        if (removed) *removed = found;
+        return SVO_OK;
+    }
+    uint32_t n = 0;
+    for (int depth = 0;; depth++) {
+        if (w->nodes[n].leaf) w->split(n);
+        const uint32_t slot = child_slot(wx, wy, wz, (uint32_t)(2 * (w->levels - 1 - depth)));
+        uint32_t c = w->kids(n)[slot];
+        if (!c) break;  // already empty
+        if (depth + 1 == target) {
+            if (w->nodes[c].leaf) {
+                const Material& m = w->pal.m[w->nodes[c].mat];
+                found = svo_block{m.flags, m.color, m.meta};
+            }
+            w->drop_children(c);
+            w->free_nodes.push_back(c);
+            w->live_nodes--;
+            w->kids(n)[slot] = 0;
+            break;
+        }
+        n = c;
+    }
+    if (removed) *removed = found;
+    return SVO_OK;
+}
+
+// initTetraHexaTree's debug blocks (tetrahexa_tree.cpp:20-27)
+extern "C" int svo_init_tetra_hexa_tree(svo_world* w) {
+    if (!w) SVO_FAIL(SVO_EINVAL, "svo_init_tetra_hexa_tree: NULL world");
+    struct P {
+        int x, y, z;
+        uint32_t f;
+        int level;
+    } puts[8] = {{1000, 1000, 1000, 1, 5}, {10, 100, 10, 2, 6}, {100, 10, 100, 3, 6}, {20, 10, 200, 4, 5},
+                 {1, 10, 10, 5, 6},        {2, 10, 10, 6, 6},    {3, 10, 10, 7, 6},    {4, 10, 10, 8, 6}};
+    // the reference's levels are for maxDepth 6; rescale so "6" stays one voxel
+    for (auto& p : puts) {
+        svo_block b{p.f, 0ull, 0.0f};
+        int lv = p.level + (w->levels - 5);
+        if (lv < 1) lv = 1;
+        int rc = svo_put_block(w, p.x, p.y, p.z, &b, lv);
+        if (rc) return rc;
+    }
+    return SVO_OK;
+}
+
+namespace {
+struct TerrainIds {
+    uint16_t water, grass, dirt, stone;
+};
+}  // namespace
+
+// genWorld (world_gen.cpp:13-42) over width x length columns
+extern "C" int svo_gen_world(svo_world* w, int32_t width, int32_t length) {
+    if (!w || width < 0 || length < 0) SVO_FAIL(SVO_EINVAL, "svo_gen_world: bad argument");
+    Simplex2 n42, n64, n100;
+    simplex2_seed(n42, 42);
+    simplex2_seed(n64, 64);
+    simplex2_seed(n100, 100);
+    const uint64_t green = rgb_to_u64(0, 150, 10), brown = rgb_to_u64(45, 18, 0), grey = rgb_to_u64(33, 33, 33);
+    const int32_t voxel = w->levels + 1;
+    auto id = [&](uint32_t f, uint64_t c) { return (uint16_t)w->pal.intern(Material{1u | f, c, 0.0f}); };
+    for (int32_t x = 0; x < width; x++) {
+        for (int32_t z = 0; z < length; z++) {
+            int32_t y = terrain_height(n42.perm, n64.perm, n100.perm, x, z);
+            if (y < 20) {
+                uint16_t water = id(0x4u | 0x10u, green);
+                for (int32_t i = 20; i > y; i--) put_block_id(w, x, i, z, water, voxel);
+                put_block_id(w, x, y, z, id(0, brown), voxel);
+            } else {
+                put_block_id(w, x, y, z, id(0, green), voxel);
+            }
+            y--;
+            for (int i = 3; y > 0 && i; i--, y--) put_block_id(w, x, y, z, id(0, brown), voxel);
+            for (; y > 0; y--) put_block_id(w, x, y, z, id(0, grey), voxel);
+        }
+    }
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Canonical linearisation.  Region classes in the solid view (non-solid blocks count as empty):
+//   EMPTY, SOLID(material), MIXED.  A MIXED region at depth levels-1 becomes a BRICK, deeper up an
+//   INTERIOR node whose non-EMPTY children follow in breadth-first order.
+// ================================================================================================
+static constexpr uint32_t C_EMPTY = 0u;
+static constexpr uint32_t C_MIXED = 0xFFFFFFFFu;  // otherwise SOLID with material = class
+
+struct BrickOut {
+    uint64_t mask;
+    uint32_t info;
+};
+
+// fold 64 voxel classes (EMPTY or SOLID ids) into brick mask + material run
+static BrickOut make_brick(const uint32_t* vox, std::vector<uint16_t>* mats_out) {
+    uint64_t mask = 0;
+    uint32_t first = C_EMPTY;
+    bool uniform = true;
+    for (int v = 0; v < 64; v++) {
+        if (vox[v] == C_EMPTY) continue;
+        mask |= 1ull << v;
+        if (first == C_EMPTY) first = vox[v];
+        else if (vox[v] != first) uniform = false;
+    }
+    if (uniform) return BrickOut{mask, K_BRICK | K_UNIFORM | (first << 16)};
+    if (mats_out)
+        for (int v = 0; v < 64; v++)
+            if (vox[v] != C_EMPTY) mats_out->push_back((uint16_t)vox[v]);
+    return BrickOut{mask, K_BRICK};
+}
+
+static uint32_t fold_classes(const uint32_t* c) {
+    uint32_t f = c[0];
+    if (f == C_MIXED) return C_MIXED;
+    for (int i = 1; i < 64; i++)
+        if (c[i] != f) return C_MIXED;
+    return f;  // all EMPTY or all SOLID(m)
+}
+
+static void finish_tree_stats(svo_tree* t) {
+    (void)t;
+}
+
+extern "C" int svo_build(const svo_world* w, svo_tree** out) {
+    if (!w || !out) SVO_FAIL(SVO_EINVAL, "svo_build: NULL argument");
+    const int L = w->levels;
+    std::vector<uint8_t> solid(w->pal.m.size());
+    for (size_t i = 0; i < solid.size(); i++) solid[i] = material_solid(w->pal.m[i]);
+    // post-order classes of every live edit node
+    std::vector<uint32_t> cls(w->nodes.size(), C_EMPTY);
+    std::function<uint32_t(uint32_t, int)> classify = [&](uint32_t n, int depth) -> uint32_t {
+        const auto& e = w->nodes[n];
+        uint32_t c;
+        if (e.leaf) {
+            c = solid[e.mat] ? (uint32_t)e.mat : C_EMPTY;
+        } else {
+            uint32_t kc[64];
+            const uint32_t* k = w->kids(n);
+            for (int i = 0; i < 64; i++) kc[i] = k[i] ? classify(k[i], depth + 1) : C_EMPTY;
+            c = fold_classes(kc);
+        }
+        cls[n] = c;
+        return c;
+    };
+    classify(0, 0);
+
+    svo_tree* t = new (std::nothrow) svo_tree();
+    if (!t) SVO_FAIL(SVO_ENOMEM, "svo_build: out of memory");
+    t->levels = L;
+    t->palette = w->pal.m;
+    // level-synchronous emission; `cur` = edit ids of this depth's nodes (in node order)
+    std::vector<uint32_t> cur{0};
+    t->nodes.push_back(Node{0, 0, K_INTERIOR});
+    uint64_t level_base = 0;
+    for (int d = 0; d < L && !cur.empty(); d++) {
+        t->nodes_per_level[d] = cur.size();
+        std::vector<uint32_t> next;
+        uint64_t next_base = level_base + cur.size();
+        for (size_t i = 0; i < cur.size(); i++) {
+            uint32_t e = cur[i];
+            Node& nd = t->nodes[level_base + i];
+            uint32_t c = cls[e];
+            if (c == C_EMPTY) {  // only the root can be an empty node
+                nd = Node{0, 0, K_INTERIOR};
+                continue;
+            }
+            if (c != C_MIXED) {
+                nd = Node{~0ull, 0, K_SOLID | (c << 16)};
+                continue;
+            }
+            const uint32_t* k = w->kids(e);
+            if (d == L - 1) {
+                uint32_t vox[64];
+                for (int v = 0; v < 64; v++) vox[v] = k[v] ? cls[k[v]] : C_EMPTY;
+                uint32_t ref = (uint32_t)t->mats.size();
+                BrickOut b = make_brick(vox, &t->mats);
+                t->nodes[level_base + i] = Node{b.mask, (b.info & K_UNIFORM) ? 0u : ref, b.info};
+                t->n_bricks++;
+                continue;
+            }
+            uint64_t mask = 0;
+            for (int s = 0; s < 64; s++)
+                if (k[s] && cls[k[s]] != C_EMPTY) {
+                    mask |= 1ull << s;
+                    next.push_back(k[s]);
+                }
+            t->nodes[level_base + i] = Node{mask, (uint32_t)(next_base + (next.size() - __builtin_popcountll(mask))), K_INTERIOR};
+        }
+        t->nodes.resize(next_base + next.size(), Node{0, 0, 0});
+        level_base = next_base;
+        cur.swap(next);
+    }
+    if (t->nodes.size() > 0xFFFFFFFFull || t->mats.size() > 0xFFFFFFFFull) {
+        delete t;
+        SVO_FAIL(SVO_ERANGE, "svo_build: tree exceeds 2^32 nodes");
+    }
+    finish_tree_stats(t);
+    *out = t;
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Terrain builder: genWorld's columns -> canonical tree without a per-voxel edit tree.
+// Heights are generated in parallel; a min/max pyramid over aligned 4^k column footprints
+// classifies every region in O(1) (see classify_region); the tree is emitted depth by depth with a
+// count pass + prefix sum + write pass, all multi-threaded.
+// ================================================================================================
+namespace {
+struct Pyramid {
+    int32_t W, L;           // columns
+    std::vector<int32_t> dimx, dimz;
+    std::vector<std::vector<int16_t>> hmin, hmax;  // level k: ceil(W/4^k) x ceil(L/4^k), [cx*dz + cz]
+};
+
+struct TerrainCtx {
+    int32_t levels, E, W, L;
+    const int16_t* h;  // [x*L + z]
+    Pyramid pyr;
+    uint32_t id_of[5];  // terrain material -> palette id (0 for non-solid)
+};
+
+inline uint32_t solid_class(const TerrainCtx& T, int32_t h, int32_t y) {
+    return T.id_of[terrain_material(h, y)];
+}
+
+// class of the aligned region [x0,x0+s) x [y0,y0+s) x [z0,z0+s), s = 4^k >= 4
+uint32_t classify_region(const TerrainCtx& T, int32_t x0, int32_t y0, int32_t z0, int32_t s, int k) {
+    const int32_t y1 = y0 + s - 1;
+    if (x0 >= T.W || z0 >= T.L) return C_EMPTY;  // no columns here
+    const bool partial = (x0 + s > T.W) || (z0 + s > T.L);
+    const int32_t cx = x0 >> (2 * k), cz = z0 >> (2 * k);
+    const size_t ci = (size_t)cx * T.pyr.dimz[k] + cz;
+    const int32_t hmin = T.pyr.hmin[k][ci], hmax = T.pyr.hmax[k][ci];
+    if (y1 < 1 || y0 > hmax) return C_EMPTY;
+    if (partial) return C_MIXED;
+    if (y0 >= 1 && y1 <= hmin - 4) return T.id_of[TM_STONE];
+    if (hmin != hmax) return C_MIXED;  // dirt / grass runs are < 4 voxels unless all columns agree
+    const int32_t h = hmin;
+    const uint32_t c0 = solid_class(T, h, y0);
+    const int32_t cand[4] = {1, h - 3, h, h + 1};
+    for (int i = 0; i < 4; i++) {
+        const int32_t b = cand[i];
+        if (b > y0 && b <= y1 && solid_class(T, h, b) != solid_class(T, h, b - 1)) return C_MIXED;
+    }
+    return c0;
+}
+
+void brick_voxels(const TerrainCtx& T, int32_t x0, int32_t y0, int32_t z0, uint32_t vox[64]) {
+    for (int lz = 0; lz < 4; lz++)
+        for (int lx = 0; lx < 4; lx++) {
+            const int32_t x = x0 + lx, z = z0 + lz;
+            const bool have = x < T.W && z < T.L;
+            const int32_t h = have ? T.h[(size_t)x * T.L + z] : 0;
+            for (int ly = 0; ly < 4; ly++) vox[(lz << 4) | (ly << 2) | lx] = have ? solid_class(T, h, y0 + ly) : C_EMPTY;
+        }
+}
+
+struct Region {
+    int32_t x0, y0, z0;
+};
+}  // namespace
+
+extern "C" int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out) {
+    if (!out) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: out is NULL");
+    if (levels < 2 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: levels must be in [2, 7]");
+    const int32_t E = 1 << (2 * levels);
+    if (width < 1 || length < 1 || width > E || length > E) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: columns must fit the extent");
+    TerrainCtx T;
+    T.levels = levels;
+    T.E = E;
+    T.W = width;
+    T.L = length;
+    // ---- heights (world_gen.cpp:22), parallel over x
+    std::vector<int16_t> hg((size_t)width * length);
+    {
+        Simplex2 n42, n64, n100;
+        simplex2_seed(n42, 42);
+        simplex2_seed(n64, 64);
+        simplex2_seed(n100, 100);
+        std::atomic<int> bad(0);
+        parallel_for(width, nthreads, [&](int64_t b, int64_t e) {
+            for (int64_t x = b; x < e; x++)
+                for (int32_t z = 0; z < length; z++) {
+                    int32_t h = terrain_height(n42.perm, n64.perm, n100.perm, (int32_t)x, z);
+                    if (h < 1 || h + 1 >= E || 21 >= E || h > 32767) bad = 1;
+                    hg[(size_t)x * length + z] = (int16_t)h;
+                }
+        });
+        if (bad) SVO_FAIL(SVO_ERANGE, "svo_build_terrain: a column top falls outside [1, extent-2] (wrap not supported here; use svo_gen_world)");
+    }
+    T.h = hg.data();
+    // ---- min/max pyramid over aligned 4^k footprints
+    T.pyr.W = width;
+    T.pyr.L = length;
+    T.pyr.dimx.push_back(width);
+    T.pyr.dimz.push_back(length);
+    T.pyr.hmin.push_back(hg);
+    T.pyr.hmax.push_back(hg);
+    for (int k = 1; k <= levels; k++) {
+        const int32_t px = T.pyr.dimx[k - 1], pz = T.pyr.dimz[k - 1];
+        const int32_t dx = (px + 3) / 4, dz = (pz + 3) / 4;
+        std::vector<int16_t> mn((size_t)dx * dz), mx((size_t)dx * dz);
+        const auto& pmn = T.pyr.hmin[k - 1];
+        const auto& pmx = T.pyr.hmax[k - 1];
+        parallel_for(dx, nthreads, [&](int64_t b, int64_t e) {
+            for (int64_t cx = b; cx < e; cx++)
+                for (int32_t cz = 0; cz < dz; cz++) {
+                    int16_t a = 32767, c = -32768;
+                    for (int i = 0; i < 4; i++)
+                        for (int j = 0; j < 4; j++) {
+                            const int64_t sx = cx * 4 + i, sz = (int64_t)cz * 4 + j;
+                            if (sx >= px || sz >= pz) continue;
+                            a = std::min(a, pmn[(size_t)sx * pz + sz]);
+                            c = std::max(c, pmx[(size_t)sx * pz + sz]);
+                        }
+                    mn[(size_t)cx * dz + cz] = a;
+                    mx[(size_t)cx * dz + cz] = c;
+                }
+        });
+        T.pyr.dimx.push_back(dx);
+        T.pyr.dimz.push_back(dz);
+        T.pyr.hmin.push_back(std::move(mn));
+        T.pyr.hmax.push_back(std::move(mx));
+    }
+    svo_tree* t = new (std::nothrow) svo_tree();
+    if (!t) SVO_FAIL(SVO_ENOMEM, "svo_build_terrain: out of memory");
+    t->levels = levels;
+    // palette: the blocks genWorld stores (stored flags = 1 | Block.flags)
+    t->palette.push_back(Material{0, ~0ull, 0.0f});
+    t->palette.push_back(Material{1u, rgb_to_u64(0, 150, 10), 0.0f});  // 1 grass
+    t->palette.push_back(Material{1u, rgb_to_u64(45, 18, 0), 0.0f});   // 2 dirt
+    t->palette.push_back(Material{1u, rgb_to_u64(33, 33, 33), 0.0f});  // 3 stone
+    t->palette.push_back(Material{1u | 0x14u, rgb_to_u64(0, 150, 10), 0.0f});  // 4 water (LIQUID)
+    T.id_of[TM_AIR] = C_EMPTY;
+    T.id_of[TM_WATER] = C_EMPTY;
+    T.id_of[TM_GRASS] = 1;
+    T.id_of[TM_DIRT] = 2;
+    T.id_of[TM_STONE] = 3;
+
+    // root
+    const uint32_t rc = classify_region(T, 0, 0, 0, E, levels);
+    if (rc == C_EMPTY) {
+        t->nodes.push_back(Node{0, 0, K_INTERIOR});
+        t->nodes_per_level[0] = 1;
+        *out = t;
+        return SVO_OK;
+    }
+    if (rc != C_MIXED) {
+        t->nodes.push_back(Node{~0ull, 0, K_SOLID | (rc << 16)});
+        t->nodes_per_level[0] = 1;
+        *out = t;
+        return SVO_OK;
+    }
+    std::vector<Region> cur{{0, 0, 0}};
+    std::vector<uint64_t> cur_node{0};  // node index of each MIXED region
+    t->nodes.push_back(Node{0, 0, K_INTERIOR});
+    t->nodes_per_level[0] = 1;
+    uint64_t level_end = 1;  // nodes emitted so far = start of the next depth
+    for (int d = 0; d < levels && !cur.empty(); d++) {
+        const int32_t s = 1 << (2 * (levels - d));  // region size at depth d
+        const int32_t cs = s >> 2;
+        const int64_t nr = (int64_t)cur.size();
+        if (d == levels - 1) {
+            // bricks: two passes for the material run offsets
+            std::vector<uint32_t> nmat(nr);
+            std::vector<BrickOut> bo(nr);
+            parallel_for(nr, nthreads, [&](int64_t b, int64_t e) {
+                uint32_t vox[64];
+                for (int64_t i = b; i < e; i++) {
+                    brick_voxels(T, cur[i].x0, cur[i].y0, cur[i].z0, vox);
+                    bo[i] = make_brick(vox, nullptr);
+                    nmat[i] = (bo[i].info & K_UNIFORM) ? 0u : (uint32_t)__builtin_popcountll(bo[i].mask);
+                }
+            });
+            std::vector<uint64_t> moff(nr + 1, 0);
+            for (int64_t i = 0; i < nr; i++) moff[i + 1] = moff[i] + nmat[i];
+            t->mats.resize(moff[nr]);
+            parallel_for(nr, nthreads, [&](int64_t b, int64_t e) {
+                uint32_t vox[64];
+                for (int64_t i = b; i < e; i++) {
+                    uint32_t ref = 0;
+                    if (nmat[i]) {
+                        brick_voxels(T, cur[i].x0, cur[i].y0, cur[i].z0, vox);
+                        uint64_t o = moff[i];
+                        for (int v = 0; v < 64; v++)
+                            if (vox[v] != C_EMPTY) t->mats[o++] = (uint16_t)vox[v];
+                        ref = (uint32_t)moff[i];
+                    }
+                    t->nodes[cur_node[i]] = Node{bo[i].mask, ref, bo[i].info};
+                }
+            });
+            t->n_bricks = (uint64_t)nr;
+            break;
+        }
+        // pass 1: per region, count non-empty and mixed children
+        std::vector<uint32_t> nkid(nr), nmix(nr);
+        parallel_for(nr, nthreads, [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; i++) {
+                uint32_t a = 0, m = 0;
+                for (int sl = 0; sl < 64; sl++) {
+                    uint32_t c = classify_region(T, cur[i].x0 + (sl & 3) * cs, cur[i].y0 + ((sl >> 2) & 3) * cs,
+                                                 cur[i].z0 + ((sl >> 4) & 3) * cs, cs, levels - d - 1);
+                    a += c != C_EMPTY;
+                    m += c == C_MIXED;
+                }
+                nkid[i] = a;
+                nmix[i] = m;
+            }
+        });
+        std::vector<uint64_t> koff(nr + 1, 0), moff(nr + 1, 0);
+        for (int64_t i = 0; i < nr; i++) {
+            koff[i + 1] = koff[i] + nkid[i];
+            moff[i + 1] = moff[i] + nmix[i];
+        }
+        const uint64_t base = level_end;
+        t->nodes.resize(base + koff[nr]);
+        t->nodes_per_level[d + 1] = koff[nr];
+        std::vector<Region> next(moff[nr]);
+        std::vector<uint64_t> next_node(moff[nr]);
+        // pass 2: write this depth's INTERIOR nodes and the next depth's SOLID children
+        parallel_for(nr, nthreads, [&](int64_t b, int64_t e) {
+            for (int64_t i = b; i < e; i++) {
+                uint64_t mask = 0, kpos = base + koff[i], mpos = moff[i];
+                for (int sl = 0; sl < 64; sl++) {
+                    const int32_t x = cur[i].x0 + (sl & 3) * cs, y = cur[i].y0 + ((sl >> 2) & 3) * cs,
+                                  z = cur[i].z0 + ((sl >> 4) & 3) * cs;
+                    uint32_t c = classify_region(T, x, y, z, cs, levels - d - 1);
+                    if (c == C_EMPTY) continue;
+                    mask |= 1ull << sl;
+                    if (c == C_MIXED) {
+                        next[mpos] = Region{x, y, z};
+                        next_node[mpos] = kpos;
+                        mpos++;
+                    } else {
+                        t->nodes[kpos] = Node{~0ull, 0, K_SOLID | (c << 16)};
+                    }
+                    kpos++;
+                }
+                t->nodes[cur_node[i]] = Node{mask, (uint32_t)(base + koff[i]), K_INTERIOR};
+            }
+        });
+        level_end = base + koff[nr];
+        cur.swap(next);
+        cur_node.swap(next_node);
+    }
+    if (t->nodes.size() > 0xFFFFFFFFull) {
+        delete t;
+        SVO_FAIL(SVO_ERANGE, "svo_build_terrain: tree exceeds 2^32 nodes");
+    }
+    *out = t;
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Tree queries
+// ================================================================================================
+extern "C" int svo_tree_get_info(const svo_tree* t, svo_tree_info* o) {
+    if (!t || !o) SVO_FAIL(SVO_EINVAL, "svo_tree_get_info: NULL argument");
+    memset(o, 0, sizeof(*o));
+    o->levels = t->levels;
+    o->n_materials = (uint32_t)t->palette.size();
+    o->n_nodes = t->nodes.size();
+    o->n_mat_bytes = t->mats.size() * sizeof(uint16_t);
+    o->n_bricks = t->n_bricks;
+    for (int i = 0; i < 8; i++) o->nodes_per_level[i] = t->nodes_per_level[i];
+    o->device_bytes = t->device_bytes;
+    o->device = t->device;
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_palette(const svo_tree* t, uint32_t id, svo_block* out) {
+    if (!t || !out) SVO_FAIL(SVO_EINVAL, "svo_tree_palette: NULL argument");
+    if (id >= t->palette.size()) SVO_FAIL(SVO_ERANGE, "svo_tree_palette: id out of range");
+    const Material& m = t->palette[id];
+    *out = svo_block{m.flags, m.color, m.meta};
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32_t z, svo_block* out, uint32_t* mid) {
+    if (!t || !out) SVO_FAIL(SVO_EINVAL, "svo_tree_get_block: NULL argument");
+    const uint32_t mk = (1u << (2 * t->levels)) - 1u;
+    const uint32_t wx = (uint32_t)x & mk, wy = (uint32_t)y & mk, wz = (uint32_t)z & mk;
+    uint32_t ni = 0, mat = 0;
+    for (int d = 0; d < t->levels; d++) {
+        const Node& n = t->nodes[ni];
+        const uint32_t kind = node_kind(n.info);
+        if (kind == K_SOLID) {
+            mat = node_material(n.info);
+            break;
+        }
+        if (kind == K_BRICK) {
+            const uint32_t v = child_slot(wx, wy, wz, 0);
+            if ((n.mask >> v) & 1ull)
+                mat = (n.info & K_UNIFORM) ? node_material(n.info) : t->mats[n.ref + __builtin_popcountll(n.mask & ((1ull << v) - 1ull))];
+            break;
+        }
+        const uint32_t sl = child_slot(wx, wy, wz, (uint32_t)(2 * (t->levels - 1 - d)));
+        if (!((n.mask >> sl) & 1ull)) break;
+        ni = n.ref + (uint32_t)__builtin_popcountll(n.mask & ((1ull << sl) - 1ull));
+    }
+    const Material& m = t->palette[mat];
+    *out = svo_block{m.flags, m.color, m.meta};
+    if (mid) *mid = mat;
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nb, void* mats, uint64_t mb) {
+    if (!t) SVO_FAIL(SVO_EINVAL, "svo_tree_export: NULL tree");
+    if (nodes) {
+        if (nb < t->nodes.size() * sizeof(Node)) SVO_FAIL(SVO_ERANGE, "svo_tree_export: node buffer too small");
+        memcpy(nodes, t->nodes.data(), t->nodes.size() * sizeof(Node));
+    }
+    if (mats) {
+        if (mb < t->mats.size() * sizeof(uint16_t)) SVO_FAIL(SVO_ERANGE, "svo_tree_export: material buffer too small");
+        memcpy(mats, t->mats.data(), t->mats.size() * sizeof(uint16_t));
+    }
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Host helpers (the same code the kernel runs)
+// ================================================================================================
+extern "C" int svo_proj_plane(int32_t width, int32_t height, float* ppx, float* ppy) {
+    if (width <= 0 || height <= 0 || !ppx || !ppy) SVO_FAIL(SVO_EINVAL, "svo_proj_plane: bad argument");
+    // main.cpp:94: glm::tan(glm::radians(45.0)) in double, then the float uniforms
+    const double t = tan(45.0 * 0.01745329251994329576923690768489);
+    *ppx = (float)t;
+    *ppy = (float)(t * (double)(float)height / (double)width);
+    return SVO_OK;
+}
+
+extern "C" int svo_normalize(const float v[3], float o[3]) {
+    if (!v || !o) SVO_FAIL(SVO_EINVAL, "svo_normalize: NULL argument");
+    normalize3(v, o);
+    return SVO_OK;
+}
+
+extern "C" int svo_pixel_dir(const float cam[3], float ppx, float ppy, int32_t w, int32_t h, int32_t px, int32_t py, float o[3]) {
+    if (!cam || !o || w <= 0 || h <= 0) SVO_FAIL(SVO_EINVAL, "svo_pixel_dir: bad argument");
+    RayGen g;
+    raygen_init(g, cam, ppx, ppy, w, h);
+    raygen_pixel(g, px, py, o);
+    return SVO_OK;
+}
+
+extern "C" int svo_pixel_dirs(const float cam[3], float ppx, float ppy, int32_t w, int32_t h, float* out) {
+    if (!cam || !out || w <= 0 || h <= 0) SVO_FAIL(SVO_EINVAL, "svo_pixel_dirs: bad argument");
+    RayGen g;
+    raygen_init(g, cam, ppx, ppy, w, h);
+    parallel_for(h, 0, [&](int64_t b, int64_t e) {
+        for (int64_t py = b; py < e; py++)
+            for (int32_t px = 0; px < w; px++) raygen_pixel(g, px, (int32_t)py, out + 3 * ((size_t)py * w + px));
+    });
+    return SVO_OK;
+}
+
+extern "C" int svo_noise2(int64_t seed, const double* x, const double* y, int64_t n, double* out) {
+    if ((!x || !y || !out) && n > 0) SVO_FAIL(SVO_EINVAL, "svo_noise2: NULL argument");
+    Simplex2 s;
+    simplex2_seed(s, seed);
+    for (int64_t i = 0; i < n; i++) out[i] = simplex2_eval(s.perm, x[i], y[i]);
+    return SVO_OK;
+}
+
+extern "C" int svo_terrain_heights(int32_t width, int32_t length, int32_t nthreads, int32_t* out) {
+    if (width < 0 || length < 0 || (!out && (int64_t)width * length > 0)) SVO_FAIL(SVO_EINVAL, "svo_terrain_heights: bad argument");
+    Simplex2 n42, n64, n100;
+    simplex2_seed(n42, 42);
+    simplex2_seed(n64, 64);
+    simplex2_seed(n100, 100);
+    parallel_for(width, nthreads, [&](int64_t b, int64_t e) {
+        for (int64_t x = b; x < e; x++)
+            for (int32_t z = 0; z < length; z++) out[(size_t)x * length + z] = terrain_height(n42.perm, n64.perm, n100.perm, (int32_t)x, z);
+    });
+    return SVO_OK;
+}
+
+extern "C" int svo_get_blocks(const svo_world* w, const int32_t* xyz, int64_t n, svo_block* out) {
+    if (!w || ((!xyz || !out) && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_get_blocks: NULL argument");
+    for (int64_t i = 0; i < n; i++) {
+        int rc = svo_get_block(w, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], &out[i]);
+        if (rc) return rc;
+    }
+    return SVO_OK;
+}
+
+extern "C" int svo_put_blocks(svo_world* w, const int32_t* xyz, const svo_block* b, int64_t n, int32_t level) {
+    if (!w || ((!xyz || !b) && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_put_blocks: NULL argument");
+    for (int64_t i = 0; i < n; i++) {
+        int rc = svo_put_block(w, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], &b[i], level);
+        if (rc) return rc;
+    }
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_t n, uint32_t* ids) {
+    if (!t || ((!xyz || !ids) && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_tree_get_blocks: NULL argument");
+    for (int64_t i = 0; i < n; i++) {
+        svo_block b;
+        int rc = svo_tree_get_block(t, xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], &b, &ids[i]);
+        if (rc) return rc;
+    }
+    return SVO_OK;
+}
+
+extern "C" int svo_cast_count(const svo_cast_desc* d, int64_t* n) {
+    if (!d || !n) SVO_FAIL(SVO_EINVAL, "svo_cast_count: NULL argument");
+    if (d->ray_dirs) {
+        *n = d->n_rays;
+        return SVO_OK;
+    }
+    if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0)
+        SVO_FAIL(SVO_EINVAL, "svo_cast_count: bad frame geometry");
+    const int32_t tile_rows = (d->height + 7) / 8;
+    int64_t rows = 0;
+    for (int32_t r = d->tile_row_start; r < tile_rows; r += d->tile_row_step) rows += std::min(8, d->height - r * 8);
+    *n = rows * d->width;
+    return SVO_OK;
+}

@@ -1,0 +1,246 @@
+"""GPU parity: the gfx950 cast kernel (through the C ABI) against the oracle's restatement of
+castRayFromCam (src/ray_caster.cpp:54-87) on the same inputs.
+
+Bar: bit-exact voxel position, lastPos, stepsLeft, hit flag and block (flags, colour); hit.t
+within 1e-5 relative (north_star) — the kernel actually reproduces it bit-exactly, which is also
+checked.  Parity domain: outside root child 63 of the reference world."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+T_RTOL = 1e-5  # north_star tolerance on hit.t
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def gtree(torch_cuda, ref_tree):
+    ref_tree.upload(0)
+    return ref_tree
+
+
+def compare(rt, tree, gpu_out, ref, label):
+    g = rt.decode_hits(gpu_out)
+    pal = tree.palette()
+    pf = np.array([p[0] for p in pal], np.uint32)
+    pc = np.array([p[1] for p in pal], np.uint64)
+    n = len(ref["hit"])
+    assert len(g["hit"]) == n, label
+    bad = np.nonzero((g["pos"] != ref["pos"]).any(1))[0]
+    assert len(bad) == 0, "%s: pos differs at %d rays, first %s gpu=%s ref=%s" % (label, len(bad), bad[:5], g["pos"][bad[:3]], ref["pos"][bad[:3]])
+    assert np.array_equal(g["hit"], ref["hit"] != 0), label
+    assert np.array_equal(g["steps"], ref["steps"]), label
+    assert np.array_equal(g["last_pos"], ref["last"]), label
+    mid = np.where(g["hit"], g["material"], 0)
+    assert np.array_equal(pf[mid], ref["flags"]) and np.array_equal(pc[mid], ref["color"]), label
+    rt_ = ref["t"].astype(np.float32)
+    gt = g["t"]
+    fin = np.isfinite(rt_)
+    assert np.array_equal(np.isnan(gt), np.isnan(rt_)), label
+    assert np.all(np.abs(gt[fin] - rt_[fin]) <= T_RTOL * np.maximum(1.0, np.abs(rt_[fin]))), label
+    assert np.array_equal(gt[fin], rt_[fin]), label + " (t not bit-exact)"
+
+
+CAMERAS = [
+    ((35.0, 50.0, 35.0), (1.0, 0.0, 1.0)),      # reference default (globals.cpp:20-21)
+    ((4.0, 90.0, 4.0), (1.0, -0.45, 1.0)),      # SURVEY.md C1 pose
+    ((100.0, 120.0, 100.0), (1.0, -1.2, 0.3)),
+    ((150.3, 44.7, 20.9), (-0.6, -0.2, 1.0)),   # fractional origin, negative x
+]
+
+
+@pytest.mark.parametrize("cam", range(len(CAMERAS)))
+@pytest.mark.parametrize("steps", [30, 300])
+def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, steps):
+    org, d = CAMERAS[cam]
+    dn = rt.normalize(d)
+    W = H = 256
+    out = gtree.cast_frame(org, dn, W, H, steps)
+    ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
+    assert ref["rc"] == 0
+    compare(rt, gtree, out, ref, "cam%d S=%d" % (cam, steps))
+
+
+def test_reference_world_1080p(rt, gtree, ref_world_oracle):
+    org, d = CAMERAS[0]
+    dn = rt.normalize(d)
+    out = gtree.cast_frame(org, dn, 1920, 1080, 300)
+    ref = ref_world_oracle.cast_frame(org, dn, 1920, 1080, 300, nthreads=16)
+    compare(rt, gtree, out, ref, "1080p")
+    g = rt.decode_hits(out)
+    assert abs(g["hit"].mean() - 0.469) < 5e-4  # SURVEY.md §6 (reference probe)
+
+
+def _explicit(rt, torch, tree, T, origins, dirs, steps):
+    dirs = np.ascontiguousarray(dirs, np.float32)
+    origins = np.ascontiguousarray(origins, np.float32)
+    gd = torch.from_numpy(dirs).cuda()
+    go = torch.from_numpy(origins).cuda()
+    out = tree.cast_rays(gd, go, steps=steps)
+    ref = {k: [] for k in ("pos", "last", "steps", "hit", "flags", "color", "t")}
+    for o, d in zip(origins, dirs):
+        r = T.cast_ray(o, d, steps)
+        assert r.err == 0
+        ref["pos"].append(list(r.pos))
+        ref["last"].append(list(r.last))
+        ref["steps"].append(r.steps)
+        ref["hit"].append(r.hit)
+        ref["flags"].append(r.flags)
+        ref["color"].append(r.color)
+        ref["t"].append(r.t)
+    ref = {k: np.array(v) for k, v in ref.items()}
+    ref["flags"] = ref["flags"].astype(np.uint32)
+    ref["color"] = ref["color"].astype(np.uint64)
+    return out, ref
+
+
+def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
+    hs = rt.terrain_heights(200, 200)
+    lake = np.argwhere(hs < 17)[0]
+    n = rt.normalize
+    cases = [
+        ((35, 50, 35), n([1, 0, 1]), 30),           # the reference pick ray: NaN deltaPos, walks z
+        ((35, 50, 35), n([1, 0, 1]), 300),
+        ((50.5, 60, 50.5), (0.0, -1.0, 0.0), 300),  # exact zero components
+        ((50.0, 60, 50.0), (0.0, -1.0, 0.0), 300),  # integral origin + zero dir: NaN on x and z
+        ((50.5, 60, 50.5), (-0.0, -1.0, -0.0), 300),  # negative zeros: step +1, delta -inf
+        ((-3.5, 40.25, -2.75), n([1, -0.3, 1]), 300),  # trunc != floor
+        ((-0.5, 45.0, 120.5), n([-1, -0.2, 0.1]), 300),
+        ((1020.5, 35.5, 50.5), n([1, -0.05, 0.01]), 300),  # wraps past 1024
+        ((30.5, 40.5, 1022.5), n([0.02, -0.1, 1]), 300),
+        ((lake[0] + 0.5, 40.5, lake[1] + 0.5), (0.0, -1.0, 0.0), 300),  # water pass-through
+        ((21.5, 30.0, 201.5), (0.0, -1.0, 0.0), 300),  # level-5 leaf, flags 5
+        ((10.5, 110.0, 10.5), (0.0, -1.0, 0.0), 300),  # reflective voxel (10,100,10), flags 3
+        ((10.5, 110.0, 10.5), (0.0, -1.0, 0.0), 10),   # hit on the last step: steps = 0
+        ((10.5, 110.0, 10.5), (0.0, -1.0, 0.0), 9),    # one short: miss
+        ((10.5, 110.0, 10.5), (0.0, -1.0, 0.0), 0),    # no step at all
+        ((10.5, 110.0, 10.5), (0.0, 0.0, 0.0), 50),    # zero direction: all NaN, walks z
+        ((12.25, 70.5, 80.75), (float("nan"), -1.0, 0.0), 50),
+        ((99.9, 33.3, 66.6), n([1e-30, -1, 1e-30]), 300),
+        ((5.5, 200.0, 5.5), n([0.3, -1, 0.2]), 300),
+    ]
+    origins = np.array([c[0] for c in cases], np.float32)
+    dirs = np.array([c[1] for c in cases], np.float32)
+    for steps in sorted(set(c[2] for c in cases)):
+        sel = [i for i, c in enumerate(cases) if c[2] == steps]
+        out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps)
+        compare(rt, gtree, out, ref, "edge S=%d" % steps)
+
+
+def test_random_rays(rt, torch_cuda, gtree, ref_world_oracle):
+    rng = np.random.default_rng(11)
+    n = 4000
+    org = np.stack([rng.uniform(-50, 250, n), rng.uniform(0, 120, n), rng.uniform(-50, 250, n)], 1).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    d[::7, 1] = 0.0  # plenty of exact zero components
+    d[::11, 0] = 0.0
+    out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, org, d, 300)
+    compare(rt, gtree, out, ref, "random")
+
+
+def test_cast_ray_from_cam_dropin(rt, gtree, ref_world_oracle):
+    for (org, d) in CAMERAS:
+        dn = rt.normalize(d)
+        for steps in (0, 1, 30, 300):
+            (pos, last, st), blk = gtree.cast_ray_from_cam(org, dn, steps)
+            r = ref_world_oracle.cast_ray(org, dn, steps)
+            assert pos == tuple(r.pos) and last == tuple(r.last) and st == r.steps
+            assert blk[:2] == (r.flags, r.color)
+
+
+def test_tile_row_sharding_reassembles(rt, torch_cuda, gtree):
+    org, d = CAMERAS[1]
+    dn = rt.normalize(d)
+    W, H = 320, 200  # 25 tile rows
+    full = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300))
+    for G in (2, 3, 4):
+        rows = np.zeros((H, W), bool)
+        for r in range(G):
+            part = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=r, tile_row_step=G))
+            tr = list(range(r, (H + 7) // 8, G))
+            py = np.concatenate([np.arange(t * 8, min(H, t * 8 + 8)) for t in tr])
+            idx = (py[:, None] * W + np.arange(W)[None, :]).ravel()
+            for k in ("pos", "steps", "material", "t"):
+                assert np.array_equal(part[k], full[k][idx]), (G, r, k)
+            rows[py] = True
+        assert rows.all()
+
+
+def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):
+    """Config C1: the reference world's [0,256)^3 as a dense grid (coordinates & 255) on the CPU
+    oracle vs the same voxels in a 4-level tree on the GPU."""
+    D = oracle_mod.Dense(ref_world_oracle, 256)
+    rc, f, c = ref_world_oracle.dump_box(0, 0, 0, 256, 256, 256)
+    nz = np.argwhere(c != np.uint64(0xFFFFFFFFFFFFFFFF))
+    w = rt.World(4)
+    pts = nz[:, ::-1]  # (z,y,x) -> (x,y,z)
+    w.put_blocks(pts, f[c != np.uint64(0xFFFFFFFFFFFFFFFF)] & ~np.uint32(1), c[c != np.uint64(0xFFFFFFFFFFFFFFFF)])
+    t = w.build().upload(0)
+    dn = rt.normalize([1, 0, 1])
+    out = rt.decode_hits(t.cast_frame((35, 50, 35), dn, 256, 256, 300))
+    ref = D.cast_frame((35, 50, 35), dn, 256, 256, 300)
+    assert np.array_equal(out["pos"], ref["pos"]) and np.array_equal(out["steps"], ref["steps"])
+    assert np.array_equal(out["hit"], ref["hit"] != 0)
+    pal = t.palette()
+    pc = np.array([p[1] for p in pal], np.uint64)
+    assert np.array_equal(pc[np.where(out["hit"], out["material"], 0)], ref["color"])
+
+
+@pytest.fixture(scope="module")
+def depth12(rt, torch_cuda):
+    t = rt.Tree.terrain(6, 4096, 4096)
+    t.upload(0)
+    return t
+
+
+def test_depth12_sampled_parity(rt, oracle_mod, depth12):
+    """C3: depth-12 terrain (4096^2 columns, 6 levels), the C1 pose, S = 16384; sampled pixels
+    against the oracle's reference-format (collapsed) tree."""
+    T = oracle_mod.Tree.terrain(6, 4096, 4096)
+    dn = rt.normalize([1, -0.45, 1])
+    W, H = 1920, 1080
+    out = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, W, H, 16384))
+    rng = np.random.default_rng(5)
+    pix = np.unique(np.concatenate([rng.integers(0, W * H, 6000), np.arange(W * 539, W * 541), np.arange(0, W), np.arange(W * (H - 1), W * H)]))
+    ref = T.cast_frame((4, 90, 4), dn, W, H, 16384, pixels=pix, nthreads=16)
+    assert ref["rc"] == 0
+    sub = {k: v[pix] for k, v in out.items()}
+    pal = depth12.palette()
+    pf = np.array([p[0] for p in pal], np.uint32)
+    pc = np.array([p[1] for p in pal], np.uint64)
+    assert np.array_equal(sub["pos"], ref["pos"])
+    assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["steps"], ref["steps"])
+    assert np.array_equal(sub["last_pos"], ref["last"])
+    mid = np.where(sub["hit"], sub["material"], 0)
+    assert np.array_equal(pf[mid], ref["flags"]) and np.array_equal(pc[mid], ref["color"])
+    assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
+    assert sub["hit"].mean() > 0.99  # every ray points down and lands on terrain
+
+
+def test_depth12_full_frame_properties(rt, depth12):
+    """Size-independent properties at the full bench size: determinism, every hit voxel is solid
+    in the tree and its predecessor is not, steps accounting."""
+    dn = rt.normalize([1, -0.45, 1])
+    a = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
+    b = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    rng = np.random.default_rng(9)
+    idx = rng.integers(0, len(a["hit"]), 20000)
+    ids = depth12.get_blocks(a["pos"][idx])
+    assert np.array_equal(ids != 0, a["hit"][idx])
+    assert np.array_equal(np.where(a["hit"][idx], a["material"][idx], 0), ids)
+    assert np.all(depth12.get_blocks(a["last_pos"][idx][a["hit"][idx]]) == 0)
+    # L1 distance from trunc(origin) to pos == steps used (one axis step per DDA step)
+    used = 16384 - a["steps"]
+    l1 = np.abs(a["pos"] - np.array([4, 90, 4])).sum(1)
+    assert np.array_equal(l1[a["hit"]], used[a["hit"]])

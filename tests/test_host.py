@@ -1,0 +1,145 @@
+"""Host side of the product (libsvo_rt.so) on CPU: the C ABI loads and exports every symbol of
+include/svo_rt.h, the world / builders / ray generation agree with the oracle, and error paths
+return status codes instead of exiting.  No kernel launches here (no GPU in the build container)."""
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def test_abi_exports_every_declared_symbol(rt):
+    hdr = open(os.path.join(ROOT, "include", "svo_rt.h")).read()
+    declared = set(re.findall(r"^\s*(?:const char\*|int|void)\s+(svo_\w+)\(", hdr, re.M))
+    assert declared == set(rt.ABI_SYMBOLS)
+    L = C.CDLL(rt.LIB_PATH)
+    for s in declared:
+        assert hasattr(L, s), s
+    assert rt.lib().svo_version() == 1
+
+
+def test_product_noise_matches_reference_golden(rt):
+    g = np.load(os.path.join(GOLD, "noise_ref.npz"))
+    for seed in np.unique(g["seed"]):
+        m = g["seed"] == seed
+        got = rt.noise2(int(seed), g["x"][m], g["y"][m])
+        assert np.array_equal(got.view(np.uint64), g["value"][m].view(np.uint64)), seed
+
+
+def test_terrain_heights_match_oracle(rt, oracle_mod):
+    assert np.array_equal(rt.terrain_heights(512, 384), oracle_mod.heights(512, 384))
+
+
+def test_world_matches_oracle_getblock(rt, ref_world, ref_world_oracle):
+    # parity domain: everything outside root child 63 ([768,1024)^3)
+    rc, f, c = ref_world_oracle.dump_box(0, 0, 0, 256, 112, 256)
+    assert rc == 0
+    zz, yy, xx = np.meshgrid(np.arange(256), np.arange(112), np.arange(256), indexing="ij")
+    pts = np.stack([xx.ravel(), yy.ravel(), zz.ravel()], 1)
+    gf, gc, _ = ref_world.get_blocks(pts)
+    assert np.array_equal(gf, f.ravel()) and np.array_equal(gc, c.ravel())
+    # wrapped and negative coordinates
+    for p in [(1034, 5, 10), (-1014, 40, 3), (5, -990, 7), (260, 30, 1300)]:
+        assert ref_world.get_block(*p)[:2] == ref_world_oracle.get_block(*p)[:2]
+
+
+def test_linearised_tree_matches_solid_view(rt, ref_tree, ref_world_oracle):
+    pal = ref_tree.palette()
+    rc, f, c = ref_world_oracle.dump_box(0, 0, 0, 256, 112, 256)
+    zz, yy, xx = np.meshgrid(np.arange(256), np.arange(112), np.arange(256), indexing="ij")
+    pts = np.stack([xx.ravel(), yy.ravel(), zz.ravel()], 1)
+    ids = ref_tree.get_blocks(pts)
+    pf = np.array([p[0] for p in pal], np.uint32)[ids]
+    pc = np.array([p[1] for p in pal], np.uint64)[ids]
+    solid = (c.ravel() != np.uint64(0xFFFFFFFFFFFFFFFF)) & ((f.ravel() & 0x10) == 0)
+    assert np.array_equal(pf[solid], f.ravel()[solid]) and np.array_equal(pc[solid], c.ravel()[solid])
+    assert np.all(ids[~solid] == 0)
+
+
+def test_terrain_builder_equals_edit_builder(rt):
+    for levels, W, L in ((4, 256, 256), (4, 200, 150), (5, 300, 1024)):
+        w = rt.World(levels)
+        w.gen_world(W, L)
+        a = w.build()
+        b = rt.Tree.terrain(levels, W, L)
+        na, ma = a.export()
+        nb, mb = b.export()
+        assert a.palette() == b.palette()
+        assert np.array_equal(na, nb) and np.array_equal(ma, mb), (levels, W, L)
+
+
+def test_raygen_bit_exact_with_oracle(rt, oracle_mod):
+    for cam, W, H in (([1, 0, 1], 256, 256), ([1, -0.45, 1], 1920, 1080), ([1, -1.2, 0.3], 640, 360), ([0, -1, 0.001], 64, 48)):
+        d = rt.normalize(cam)
+        assert np.array_equal(d.view(np.uint32), oracle_mod.normalize(cam).view(np.uint32))
+        ppx, ppy = rt.proj_plane(W, H)
+        assert (ppx, ppy) == oracle_mod.proj_plane(W, H)
+        got = rt.pixel_dirs(d, W, H)
+        rng = np.random.default_rng(W)
+        for _ in range(300):
+            px, py = int(rng.integers(0, W)), int(rng.integers(0, H))
+            ref = oracle_mod.pixel_dir(d, ppx, ppy, W, H, px, py)
+            assert np.array_equal(got[py, px].view(np.uint32), ref.view(np.uint32)), (cam, px, py)
+
+
+def test_hemisphere_golden_is_consistent():
+    g = json.load(open(os.path.join(GOLD, "hemisphere_ref.json")))
+    a = np.array(g["generator_stdout"], np.float32)
+    b = np.array(g["shader_literals"], np.float32)
+    assert a.shape == (20, 3) and np.array_equal(a, b)
+
+
+def test_put_delete_semantics(rt, oracle_mod):
+    w = rt.World(5)
+    T = oracle_mod.Tree(5)
+    T.L.orc_init_clean_root(T.h)
+    rng = np.random.default_rng(3)
+    for _ in range(400):
+        x, y, z = (int(v) for v in rng.integers(0, 64, 3))
+        lvl = int(rng.choice([6, 6, 6, 5, 4]))
+        fl = int(rng.integers(0, 32))
+        col = int(rng.integers(0, 1 << 40))
+        w.put_block(x, y, z, fl, col, 0.0, lvl)
+        T.put_block(x, y, z, fl, col, 0.0, lvl)
+    rc, f, c = T.dump_box(0, 0, 0, 64, 64, 64)
+    zz, yy, xx = np.meshgrid(np.arange(64), np.arange(64), np.arange(64), indexing="ij")
+    gf, gc, _ = w.get_blocks(np.stack([xx.ravel(), yy.ravel(), zz.ravel()], 1))
+    assert np.array_equal(gf, f.ravel()) and np.array_equal(gc, c.ravel())
+    # intended deleteBlock: the region becomes empty, neighbours keep their blocks
+    w.put_block(10, 10, 10, 0, 123, 0.0, 6)
+    w.put_block(11, 10, 10, 0, 456, 0.0, 6)
+    assert w.delete_block(10, 10, 10, 6)[1] == 123
+    assert w.get_block(10, 10, 10)[1] == 0xFFFFFFFFFFFFFFFF and w.get_block(11, 10, 10)[1] == 456
+
+
+def test_error_paths(rt):
+    h = C.c_void_p()
+    assert rt.lib().svo_world_create(0, C.byref(h)) == -1
+    assert rt.lib().svo_world_create(9, C.byref(h)) == -1
+    assert b"levels" in rt.lib().svo_last_error()
+    w = rt.World(3)
+    with pytest.raises(rt.SvoError):
+        w.put_block(0, 0, 0, 0, 1, 0.0, 9)
+    t = w.build()
+    d = rt.Tree.frame_desc([1, 1, 1], [1, 0, 0], 16, 16, 10)
+    hits = rt.Hits(None, None, None)
+    assert rt.lib().svo_cast_rays(t._h, C.byref(d), C.byref(hits), None) == -1  # NULL outputs
+    hits = rt.Hits(16, 16, 16)
+    assert rt.lib().svo_cast_rays(t._h, C.byref(d), C.byref(hits), None) == -4  # not uploaded
+    with pytest.raises(rt.SvoError):
+        rt.Tree.terrain(1, 4, 4)
+
+
+def test_cast_count_sharding(rt):
+    for H in (1080, 1077, 8, 5):
+        total = rt.Tree.count(rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 33, H, 1))
+        assert total == 33 * H
+        for step in (2, 3, 8):
+            parts = [rt.Tree.count(rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 33, H, 1, tile_row_start=s, tile_row_step=step))
+                     for s in range(step)]
+            assert sum(parts) == total

@@ -1,0 +1,95 @@
+"""The oracle (oracle/oracle.c, a CPU restatement of the reference) pinned against the golden
+vectors the reference itself produced (tests/golden/, see make_golden.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def facts():
+    return json.load(open(os.path.join(GOLD, "reference_facts.json")))
+
+
+def test_noise_matches_reference_bitwise(oracle_mod):
+    g = np.load(os.path.join(GOLD, "noise_ref.npz"))
+    for seed in np.unique(g["seed"]):
+        m = g["seed"] == seed
+        got = np.array([oracle_mod.noise2(int(seed), a, b) for a, b in zip(g["x"][m], g["y"][m])])
+        assert np.array_equal(got.view(np.uint64), g["value"][m].view(np.uint64)), seed
+
+
+def test_noise_matches_compiled_reference_live(oracle_mod):
+    # the reference's own OpenSimplexNoise.cpp, compiled into oracle/_ref (build container only)
+    if not os.path.exists("/root/reference/include/OpenSimplexNoise.cpp"):
+        pytest.skip("reference sources not present (GPU box)")
+    oracle_mod.build_ref()
+    rng = np.random.default_rng(7)
+    x, y = rng.uniform(-500, 500, 5000), rng.uniform(-500, 500, 5000)
+    ref = oracle_mod.ref_noise_batch(42, x, y)
+    got = np.array([oracle_mod.noise2(42, a, b) for a, b in zip(x, y)])
+    assert np.array_equal(ref.view(np.uint64), got.view(np.uint64))
+
+
+def test_test_cpp_known_answer(oracle_mod):
+    k = facts()["test_cpp_kat"]
+    d = oracle_mod.normalize(k["dir_unnormalized"])
+    pos = np.zeros(3, np.int32)
+    ax = oracle_mod.C.c_int32()
+    oracle_mod.lib().orc_dda_free(oracle_mod.f3(k["origin"]), d, k["steps"], pos, oracle_mod.C.byref(ax))
+    assert list(pos) == k["round"] and ax.value == k["last_hit"]
+
+
+def test_reference_world_structure(ref_world_oracle):
+    f = facts()
+    T = ref_world_oracle
+    assert T.nodes() == f["reference_world"]["nodes"]
+    assert T.arrays() == f["reference_world"]["arrays"]
+    assert T.root_bitmap() == int(f["reference_world"]["root_bitmap"], 16)
+    a, b = f["wrap"]["a"], f["wrap"]["b"]
+    assert T.get_block(*a) == T.get_block(*b)
+    for p in f["max_depth_exit"]["points"]:
+        with pytest.raises(RuntimeError):
+            T.get_block(*p)
+    lv = f["debug_blocks"]["level5_leaf"]
+    for x in range(lv["min"][0], lv["max"][0] + 1):
+        for y in range(lv["min"][1], lv["max"][1] + 1):
+            for z in range(lv["min"][2], lv["max"][2] + 1):
+                assert T.get_block(x, y, z)[0] == lv["flags"]
+    rv = f["debug_blocks"]["reflective_voxel"]
+    assert T.get_block(*rv["pos"])[0] == rv["flags"]
+
+
+def test_pick_ray_walks_z(oracle_mod, ref_world_oracle):
+    f = facts()["pick_ray_default_camera"]
+    d = oracle_mod.normalize(f["dir_unnormalized"])
+    r = ref_world_oracle.cast_ray(f["origin"], d, 30)
+    assert r.axis == f["walks_axis"] and list(r.pos) == [35, 50, 65] and r.hit == 0
+
+
+def test_default_camera_frame_statistics(oracle_mod, ref_world_oracle):
+    f = facts()["frame_default_camera"]
+    d = oracle_mod.normalize([1, 0, 1])
+    out = ref_world_oracle.cast_frame([35, 50, 35], d, f["width"], f["height"], f["steps"])
+    assert out["rc"] == 0
+    hit = out["hit"].mean()
+    steps = out["dda_steps"] / (f["width"] * f["height"])
+    assert abs(hit - f["hit_fraction"]) < f["tolerance"][0]
+    assert abs(steps - f["mean_dda_steps"]) < f["tolerance"][1]
+
+
+def test_collapse_builder_equals_putblock(oracle_mod):
+    A = oracle_mod.Tree.terrain(4, 256, 256)
+    B = oracle_mod.Tree.terrain_putblock(4, 256, 256)
+    ra, fa, ca = A.dump_box(0, 0, 0, 256, 72, 256)
+    rb, fb, cb = B.dump_box(0, 0, 0, 256, 72, 256)
+    assert ra == 0 and rb == 0
+    assert np.array_equal(fa, fb) and np.array_equal(ca, cb)
+
+
+def test_terrain_height_range(oracle_mod):
+    r = facts()["terrain_4096_height_range"]
+    h = oracle_mod.heights(4096, 4096)
+    assert h.min() == r["min"] and h.max() == r["max"]
