@@ -110,6 +110,13 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError("libsvo_rt.so not built: run `python -m raytracing_test_amd.build` (or __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1.  If
+    # torch is importable it must be loaded first, so that libsvo_rt.so binds to that runtime instead
+    # of pulling /opt/rocm's copy next to it (two runtimes on one KFD: "no ROCm-capable device").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32, f32 = C.c_void_p, C.c_int32, C.c_float
     f3 = C.POINTER(C.c_float)
