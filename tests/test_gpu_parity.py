@@ -96,9 +96,8 @@ def _explicit(rt, torch, tree, T, origins, dirs, steps):
         ref["flags"].append(r.flags)
         ref["color"].append(r.color)
         ref["t"].append(r.t)
-    ref = {k: np.array(v) for k, v in ref.items()}
-    ref["flags"] = ref["flags"].astype(np.uint32)
-    ref["color"] = ref["color"].astype(np.uint64)
+    dt = {"flags": np.uint32, "color": np.uint64, "t": np.float64}
+    ref = {k: np.array(v, dtype=dt.get(k, np.int64)) for k, v in ref.items()}
     return out, ref
 
 
