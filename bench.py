@@ -104,6 +104,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cols", type=int, default=COLS)
+    ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     args = ap.parse_args()
 
     import torch
@@ -133,7 +134,8 @@ def main():
     # equal-size buffers on every rank (RCCL gather): the largest shard's record count
     max_local = max(rt.Tree.count(rt.Tree.frame_desc(ORIGIN, cam, W, H, STEPS, ppx, ppy, r, world)) for r in range(world))
     for f in range(nframes):
-        d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world)
+        d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
+                               flags=rt.CAST_ITERATIVE if args.iterative else 0)
         descs.append(d)
         outs.append(rt.Tree.alloc_hits(max_local, dev))
     rays_local = sum(rt.Tree.count(d) for d in descs)

@@ -144,8 +144,12 @@ typedef struct {
     const float* ray_origins; /* optional */
     int32_t n_rays;
     int32_t steps;     /* DDA step budget per ray (castRayFromCam's `steps`) */
-    int32_t flags;     /* reserved, 0 */
+    int32_t flags;     /* SVO_CAST_* bits, 0 = default */
 } svo_cast_desc;
+
+/* svo_cast_desc.flags: take every DDA step one at a time (disables the exact closed-form crossing
+   of empty regions; results are identical — for testing and A/B timing) */
+#define SVO_CAST_ITERATIVE 1
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

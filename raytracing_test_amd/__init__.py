@@ -31,6 +31,7 @@ MAT_MASK = 0xFFFF
 
 # Block flags (src/globals.hpp:68-74)
 NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
+CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B reference path)
 
 
 class SvoError(RuntimeError):
@@ -356,7 +357,7 @@ class Tree:
 
     # ------------------------------------------------------------------------------ casting --
     @staticmethod
-    def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1):
+    def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1, flags=0):
         if ppx is None:
             ppx, ppy = proj_plane(width, height)
         d = CastDesc()
@@ -365,6 +366,7 @@ class Tree:
         d.width, d.height, d.ppx, d.ppy = width, height, ppx, ppy
         d.tile_row_start, d.tile_row_step = tile_row_start, tile_row_step
         d.steps = steps
+        d.flags = flags
         return d
 
     @staticmethod
@@ -390,8 +392,8 @@ class Tree:
         _check(lib().svo_cast_rays(self._h, C.byref(desc), C.byref(h), C.c_void_p(s) if s else None), "svo_cast_rays")
 
     def cast_frame(self, origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1,
-                   out=None, stream=None, sync=True):
-        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step)
+                   out=None, stream=None, sync=True, flags=0):
+        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step, flags)
         n = self.count(d)
         if out is None:
             out = self.alloc_hits(n, self.info().device)
@@ -400,7 +402,7 @@ class Tree:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return out
 
-    def cast_rays(self, dirs, origins=None, steps=300, origin=(0.0, 0.0, 0.0), out=None, stream=None, sync=True):
+    def cast_rays(self, dirs, origins=None, steps=300, origin=(0.0, 0.0, 0.0), out=None, stream=None, sync=True, flags=0):
         """Explicit rays: dirs / origins are (n, 3) float32 device tensors."""
         d = CastDesc()
         d.origin[:] = [float(x) for x in origin]
@@ -408,6 +410,7 @@ class Tree:
         d.ray_origins = origins.data_ptr() if origins is not None else None
         d.n_rays = dirs.shape[0]
         d.steps = steps
+        d.flags = flags
         if out is None:
             out = self.alloc_hits(d.n_rays, self.info().device)
         self.cast(d, out, stream)

@@ -46,6 +46,7 @@ struct CastParams {
     uint32_t wmask;
     int32_t mode;
     int32_t steps;
+    int32_t flags;
     // frame mode
     RayGen rg;
     float org[3];
@@ -69,102 +70,283 @@ struct Hit {
     uint32_t info;
 };
 
-// One ray, castRayFromCam semantics.  Region cache: (cwx,cwy,cwz) >> cshift identifies the region
-// the last lookup ended in: an empty child region (no memory access while inside it) or a brick
-// (solid mask in registers).
+// ------------------------------------------------------------------------------------------------
+// Exact closed-form skipping.  castRayFromCam's axis choice (ray_caster.cpp:71-80) is, for non-NaN
+// values, the lexicographic minimum of (T_axis, rank) with rank z < y < x: x wins only when
+// strictly smallest, y beats z only when strictly smaller.  Each axis' crossings form the sequence
+// T, T+a, T+2a, ... (deltaPos += absDelta).  absDelta is an f32 reciprocal widened to f64, so it
+// carries 24 significant bits; when every partial sum a ray can reach (<= budget+2 terms) stays
+// below 2^(lsb+53) — lsb = lowest set bit of T and a — every sum is exact and T + k*a computed
+// directly equals the k-fold accumulation bit for bit.  Such a ray ("fast") crosses an empty
+// region in O(1): the first event to leave the region is the lexicographic minimum of the three
+// per-axis exit events, and the events before it on the other axes are counted by division
+// (with an exact +-1 fix-up).  Rays that fail the test step voxel by voxel (still without memory
+// traffic inside known-empty regions).  Both paths give identical results (tests).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int dbl_lsb(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int ef = (int)((b >> 52) & 0x7FF);
+    uint64_t m = b & 0xFFFFFFFFFFFFFull;
+    if (ef == 0) return m ? -1074 + __builtin_ctzll(m) : (1 << 20);
+    return ef - 1075 + __builtin_ctzll(m | (1ull << 52));
+}
+
+__device__ __forceinline__ int dbl_ilogb(double x) {  // x > 0, normal
+    return (int)(((uint64_t)__double_as_longlong(x) >> 52) & 0x7FF) - 1023;
+}
+
+__device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
+    if (!__builtin_isfinite(T) || !__builtin_isfinite(a) || !(a > 0.0)) return false;
+    const int u = min(dbl_lsb(T), dbl_lsb(a));
+    const double bound = __builtin_fabs(T) + (double)(budget + 2) * a;
+    return dbl_ilogb(bound) + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
+}
+
+// #{ j >= 0 : T + j*a < V }  and  #{ j >= 0 : T + j*a <= V }   (exact under exact_axis)
+__device__ __forceinline__ int32_t count_lt(double T, double a, double inva, double V) {
+    if (!(T < V)) return 0;
+    int32_t k = max(1, (int32_t)__builtin_ceil((V - T) * inva));
+    while (T + (double)k * a < V) k++;
+    while (k > 1 && T + (double)(k - 1) * a >= V) k--;
+    return k;
+}
+__device__ __forceinline__ int32_t count_le(double T, double a, double inva, double V) {
+    if (T > V) return 0;
+    int32_t k = max(1, (int32_t)__builtin_floor((V - T) * inva) + 1);
+    while (T + (double)k * a <= V) k++;
+    while (k > 1 && T + (double)(k - 1) * a > V) k--;
+    return k;
+}
+
+struct Ray {
+    int32_t rx, ry, rz;
+    double tx, ty, tz;  // next crossing per axis (deltaPos)
+    double ax, ay, az;  // absDelta
+    int32_t sx, sy, sz;
+    int32_t steps;
+    uint32_t axis;
+    double tlast;
+};
+
+// one DDA step (ray_caster.cpp:70-80)
+__device__ __forceinline__ void dda_step(Ray& R) {
+    const bool cx = (R.tx < R.ty) && (R.tx < R.tz);
+    const bool cy = !cx && (R.ty < R.tz);
+    if (cx) {
+        R.rx += R.sx;
+        R.tlast = R.tx;
+        R.tx += R.ax;
+        R.axis = 0u;
+    } else if (cy) {
+        R.ry += R.sy;
+        R.tlast = R.ty;
+        R.ty += R.ay;
+        R.axis = 1u;
+    } else {
+        R.rz += R.sz;
+        R.tlast = R.tz;
+        R.tz += R.az;
+        R.axis = 2u;
+    }
+    R.steps--;
+}
+
+// steps along one axis until the wrapped coordinate w leaves its aligned 2^sh cell
+__device__ __forceinline__ int32_t exit_steps(uint32_t w, int32_t s, uint32_t sh) {
+    const uint32_t lo = w & ~((1u << sh) - 1u);
+    return s > 0 ? (int32_t)(lo + (1u << sh) - w) : (int32_t)(w - lo + 1u);
+}
+
+// Cross the empty aligned cell of size 2^sh containing the current voxel in one move.  Returns
+// false (state unchanged) when the budget ends inside the cell.
+__device__ __forceinline__ bool skip_cell(Ray& R, uint32_t wx, uint32_t wy, uint32_t wz, uint32_t sh, double iax, double iay,
+                                          double iaz) {
+    const int32_t lim = R.steps + 1;  // exits beyond the budget are clamped (safe: total > steps)
+    const int32_t ex = min(exit_steps(wx, R.sx, sh), lim);
+    const int32_t ey = min(exit_steps(wy, R.sy, sh), lim);
+    const int32_t ez = min(exit_steps(wz, R.sz, sh), lim);
+    const double Ex = R.tx + (double)(ex - 1) * R.ax;
+    const double Ey = R.ty + (double)(ey - 1) * R.ay;
+    const double Ez = R.tz + (double)(ez - 1) * R.az;
+    int32_t cx, cy, cz, total;
+    if ((Ex < Ey) && (Ex < Ez)) {  // x leaves first; y, z events tied with it come before it
+        cy = count_le(R.ty, R.ay, iay, Ex);
+        cz = count_le(R.tz, R.az, iaz, Ex);
+        total = ex + cy + cz;
+        if (total > R.steps) return false;
+        R.rx += R.sx * ex;
+        R.ry += R.sy * cy;
+        R.rz += R.sz * cz;
+        R.ty += (double)cy * R.ay;
+        R.tz += (double)cz * R.az;
+        R.tlast = Ex;
+        R.tx = Ex + R.ax;
+        R.axis = 0u;
+    } else if (Ey < Ez) {  // y first; tied x events come after it, tied z events before
+        cx = count_lt(R.tx, R.ax, iax, Ey);
+        cz = count_le(R.tz, R.az, iaz, Ey);
+        total = ey + cx + cz;
+        if (total > R.steps) return false;
+        R.rx += R.sx * cx;
+        R.ry += R.sy * ey;
+        R.rz += R.sz * cz;
+        R.tx += (double)cx * R.ax;
+        R.tz += (double)cz * R.az;
+        R.tlast = Ey;
+        R.ty = Ey + R.ay;
+        R.axis = 1u;
+    } else {  // z first; tied x and y events come after it
+        cx = count_lt(R.tx, R.ax, iax, Ez);
+        cy = count_lt(R.ty, R.ay, iay, Ez);
+        total = ez + cx + cy;
+        if (total > R.steps) return false;
+        R.rx += R.sx * cx;
+        R.ry += R.sy * cy;
+        R.rz += R.sz * ez;
+        R.tx += (double)cx * R.ax;
+        R.ty += (double)cy * R.ay;
+        R.tlast = Ez;
+        R.tz = Ez + R.az;
+        R.axis = 2u;
+    }
+    R.steps -= total;
+    return true;
+}
+
+// Region lookup of a wrapped voxel: SOLID hit, an empty child cell (returns its shift), or the
+// brick holding the voxel (mask / ref / info returned).  tetrahexa_tree.cpp:124-152 on the
+// breadth-first layout.
+enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
+
+__device__ __forceinline__ uint32_t lookup(const CastParams& P, uint32_t wx, uint32_t wy, uint32_t wz, uint32_t& sh_out,
+                                           uint64_t& bmask, uint32_t& bref, uint32_t& binfo) {
+    uint32_t ni = 0u;
+    for (int32_t dd = 0; dd < P.levels; dd++) {
+        const Node n = P.nodes[ni];
+        const uint32_t kind = n.info & K_KIND_MASK;
+        if (kind == K_SOLID) {
+            binfo = n.info;
+            return R_SOLID;
+        }
+        if (kind == K_BRICK) {
+            bmask = n.mask;
+            bref = n.ref;
+            binfo = n.info;
+            sh_out = 2u;
+            return R_BRICK;
+        }
+        const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
+        const uint32_t sl = child_slot(wx, wy, wz, sh);
+        if (!((n.mask >> sl) & 1ull)) {
+            sh_out = sh;
+            return R_EMPTY;
+        }
+        ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
+    }
+    sh_out = 0u;  // malformed tree: treat as a one-voxel empty cell
+    return R_EMPTY;
+}
+
+__device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t mask, uint32_t ref, uint32_t info, uint32_t v) {
+    return (info & K_UNIFORM) ? (info >> 16) : (uint32_t)P.mats[ref + (uint32_t)__popcll(mask & ((1ull << v) - 1ull))];
+}
+
+// One ray with castRayFromCam semantics.
 __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], const float d[3]) {
-    const Dda1 ax = dda_axis(o[0], d[0]);
-    const Dda1 ay = dda_axis(o[1], d[1]);
-    const Dda1 az = dda_axis(o[2], d[2]);
-    int32_t rx = ax.cell, ry = ay.cell, rz = az.cell;
-    double tx = ax.dpos, ty = ay.dpos, tz = az.dpos;
-    int32_t steps = P.steps;
-    uint32_t axis = 3u;
-    double tlast = 0.0;
+    Ray R;
+    {
+        const Dda1 ax = dda_axis(o[0], d[0]);
+        const Dda1 ay = dda_axis(o[1], d[1]);
+        const Dda1 az = dda_axis(o[2], d[2]);
+        R.rx = ax.cell;
+        R.ry = ay.cell;
+        R.rz = az.cell;
+        R.tx = ax.dpos;
+        R.ty = ay.dpos;
+        R.tz = az.dpos;
+        R.ax = ax.adelta;
+        R.ay = ay.adelta;
+        R.az = az.adelta;
+        R.sx = ax.step;
+        R.sy = ay.step;
+        R.sz = az.step;
+    }
+    R.steps = P.steps;
+    R.axis = 3u;
+    R.tlast = 0.0;
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.tx, R.ax, P.steps) && exact_axis(R.ty, R.ay, P.steps) &&
+                      exact_axis(R.tz, R.az, P.steps);
+    const double iax = 1.0 / R.ax, iay = 1.0 / R.ay, iaz = 1.0 / R.az;
     bool hit = false;
-    uint32_t mat = 0;
-    bool cvalid = false, cbrick = false;
-    uint32_t cwx = 0, cwy = 0, cwz = 0, cshift = 0;
-    uint64_t bmask = 0;
-    uint32_t bref = 0, binfo = 0;
+    uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
-    while (steps > 0) {
-        // ray_caster.cpp:71-80
-        const bool sx = (tx < ty) && (tx < tz);
-        const bool sy = !sx && (ty < tz);
-        if (sx) {
-            rx += ax.step;
-            tlast = tx;
-            tx += ax.adelta;
-            axis = 0u;
-        } else if (sy) {
-            ry += ay.step;
-            tlast = ty;
-            ty += ay.adelta;
-            axis = 1u;
-        } else {
-            rz += az.step;
-            tlast = tz;
-            tz += az.adelta;
-            axis = 2u;
-        }
-        steps--;
-        const uint32_t wx = (uint32_t)rx & wm, wy = (uint32_t)ry & wm, wz = (uint32_t)rz & wm;
-        if (!cvalid || (((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> cshift) != 0u) {
-            // walk from the root (tetrahexa_tree.cpp:124-152 / low_res.frag:493-531)
-            cvalid = true;
-            cbrick = false;
-            cwx = wx;
-            cwy = wy;
-            cwz = wz;
-            cshift = 0u;
-            uint32_t ni = 0u;
-            for (int32_t dd = 0; dd < P.levels; dd++) {
-                const Node n = P.nodes[ni];
-                const uint32_t kind = n.info & K_KIND_MASK;
-                if (kind == K_SOLID) {
-                    hit = true;
-                    mat = n.info >> 16;
-                    break;
-                }
-                if (kind == K_BRICK) {
-                    cbrick = true;
-                    bmask = n.mask;
-                    bref = n.ref;
-                    binfo = n.info;
-                    cshift = 2u;
-                    break;
-                }
-                const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
-                const uint32_t sl = child_slot(wx, wy, wz, sh);
-                if (!((n.mask >> sl) & 1ull)) {
-                    cshift = sh;
-                    break;
-                }
-                ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
-            }
-            if (hit) break;
-        }
-        if (cbrick) {
-            const uint32_t v = child_slot(wx, wy, wz, 0u);
-            if ((bmask >> v) & 1ull) {
+    if (R.steps > 0) {
+        dda_step(R);
+        for (;;) {
+            // the voxel just entered is untested
+            uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
+            uint32_t sh = 0u, bref = 0u, binfo = 0u;
+            uint64_t bmask = 0ull;
+            const uint32_t kind = lookup(P, wx, wy, wz, sh, bmask, bref, binfo);
+            if (kind == R_SOLID) {
                 hit = true;
-                mat = (binfo & K_UNIFORM) ? (binfo >> 16) : (uint32_t)P.mats[bref + (uint32_t)__popcll(bmask & ((1ull << v) - 1ull))];
+                mat = binfo >> 16;
                 break;
             }
+            if (kind == R_BRICK) {
+                // voxel steps inside the brick, solid mask in registers
+                const uint32_t cwx = wx, cwy = wy, cwz = wz;
+                bool left = false;
+                for (;;) {
+                    const uint32_t v = child_slot(wx, wy, wz, 0u);
+                    if ((bmask >> v) & 1ull) {
+                        hit = true;
+                        mat = brick_material(P, bmask, bref, binfo, v);
+                        break;
+                    }
+                    if (R.steps <= 0) break;
+                    dda_step(R);
+                    wx = (uint32_t)R.rx & wm;
+                    wy = (uint32_t)R.ry & wm;
+                    wz = (uint32_t)R.rz & wm;
+                    if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
+                        left = true;
+                        break;
+                    }
+                }
+                if (hit || !left) break;
+                continue;
+            }
+            // empty cell of size 2^sh around the voxel
+            if (R.steps <= 0) break;
+            if (fast && skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) continue;
+            // step through the cell without lookups (budget ends inside it, or not exact)
+            const uint32_t cwx = wx, cwy = wy, cwz = wz;
+            bool left = false;
+            while (R.steps > 0) {
+                dda_step(R);
+                wx = (uint32_t)R.rx & wm;
+                wy = (uint32_t)R.ry & wm;
+                wz = (uint32_t)R.rz & wm;
+                if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> sh) != 0u) {
+                    left = true;
+                    break;
+                }
+            }
+            if (!left) break;
         }
     }
     Hit h;
-    h.x = rx;
-    h.y = ry;
-    h.z = rz;
-    h.steps_left = hit ? steps : 0;
-    h.t = (float)tlast;
+    h.x = R.rx;
+    h.y = R.ry;
+    h.z = R.rz;
+    h.steps_left = hit ? R.steps : 0;
+    h.t = (float)R.tlast;
     uint32_t neg = 0u;
-    if (axis == 0u) neg = ax.step < 0;
-    else if (axis == 1u) neg = ay.step < 0;
-    else if (axis == 2u) neg = az.step < 0;
-    h.info = (hit ? HIT_BIT : 0u) | (axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (mat & MAT_MASK);
+    if (R.axis == 0u) neg = R.sx < 0;
+    else if (R.axis == 1u) neg = R.sy < 0;
+    else if (R.axis == 2u) neg = R.sz < 0;
+    h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (mat & MAT_MASK);
     return h;
 }
 
@@ -223,6 +405,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.steps = d->steps;
+    P.flags = d->flags;
     P.org[0] = d->origin[0];
     P.org[1] = d->origin[1];
     P.org[2] = d->origin[2];

@@ -63,10 +63,11 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     org, d = CAMERAS[cam]
     dn = rt.normalize(d)
     W = H = 256
-    out = gtree.cast_frame(org, dn, W, H, steps)
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    compare(rt, gtree, out, ref, "cam%d S=%d" % (cam, steps))
+    for flags in (0, rt.CAST_ITERATIVE):
+        out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
+        compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
 
 def test_reference_world_1080p(rt, gtree, ref_world_oracle):
@@ -79,12 +80,12 @@ def test_reference_world_1080p(rt, gtree, ref_world_oracle):
     assert abs(g["hit"].mean() - 0.469) < 5e-4  # SURVEY.md §6 (reference probe)
 
 
-def _explicit(rt, torch, tree, T, origins, dirs, steps):
+def _explicit(rt, torch, tree, T, origins, dirs, steps, flags=0):
     dirs = np.ascontiguousarray(dirs, np.float32)
     origins = np.ascontiguousarray(origins, np.float32)
     gd = torch.from_numpy(dirs).cuda()
     go = torch.from_numpy(origins).cuda()
-    out = tree.cast_rays(gd, go, steps=steps)
+    out = tree.cast_rays(gd, go, steps=steps, flags=flags)
     ref = {k: [] for k in ("pos", "last", "steps", "hit", "flags", "color", "t")}
     for o, d in zip(origins, dirs):
         r = T.cast_ray(o, d, steps)
@@ -130,8 +131,9 @@ def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
     dirs = np.array([c[1] for c in cases], np.float32)
     for steps in sorted(set(c[2] for c in cases)):
         sel = [i for i, c in enumerate(cases) if c[2] == steps]
-        out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps)
-        compare(rt, gtree, out, ref, "edge S=%d" % steps)
+        for flags in (0, rt.CAST_ITERATIVE):
+            out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps, flags)
+            compare(rt, gtree, out, ref, "edge S=%d flags=%d" % (steps, flags))
 
 
 def _segment_hits_box(o, d, tmax, lo, hi):
@@ -163,8 +165,9 @@ def test_random_rays(rt, torch_cuda, gtree, ref_world_oracle):
     # octant box [-256, 0)^3 for these origins
     keep = ~_segment_hits_box(org, d, 301.0, np.full(3, -256.0), np.zeros(3))
     org, d = org[keep], d[keep]
-    out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, org, d, 300)
-    compare(rt, gtree, out, ref, "random")
+    for flags in (0, rt.CAST_ITERATIVE):
+        out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, org, d, 300, flags)
+        compare(rt, gtree, out, ref, "random flags=%d" % flags)
 
 
 def test_cast_ray_from_cam_dropin(rt, gtree, ref_world_oracle):
@@ -252,8 +255,10 @@ def test_depth12_full_frame_properties(rt, depth12):
     dn = rt.normalize([1, -0.45, 1])
     a = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
     b = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
+    c = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_ITERATIVE))
     for k in a:
         assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(a[k], c[k]), k
     rng = np.random.default_rng(9)
     idx = rng.integers(0, len(a["hit"]), 20000)
     ids = depth12.get_blocks(a["pos"][idx])
