@@ -129,22 +129,23 @@ def main():
     ppx, ppy = rt.proj_plane(W, H)
     cam = rt.normalize(CAM)
 
+    from raytracing_test_amd import shard
+
     nframes = world
-    descs, outs = [], []
-    # equal-size buffers on every rank (RCCL gather): the largest shard's record count
-    max_local = max(rt.Tree.count(rt.Tree.frame_desc(ORIGIN, cam, W, H, STEPS, ppx, ppy, r, world)) for r in range(world))
+    descs, flats, outs = [], [], []
+    # equal-size record buffers on every rank (RCCL gather): the largest shard, kernel writes in place
+    n_pad = shard.max_shard_count(W, H, world)
     for f in range(nframes):
         d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
                                flags=rt.CAST_ITERATIVE if args.iterative else 0)
         descs.append(d)
-        outs.append(rt.Tree.alloc_hits(max_local, dev))
-    rays_local = sum(rt.Tree.count(d) for d in descs)
+        flat, views = shard.alloc_flat(n_pad, torch.device("cuda", dev))
+        flats.append(flat)
+        outs.append(views)
     stream = torch.cuda.Stream(device=dev)
     gather_bufs = None
-    if world > 1 and not args.no_gather:
-        n0 = max_local
-        if rank == 0:
-            gather_bufs = [[torch.empty(n0 * 6, dtype=torch.int32, device=dev) for _ in range(world)] for _ in range(nframes)]
+    if world > 1 and not args.no_gather and rank == 0:
+        gather_bufs = [[torch.empty_like(flats[0]) for _ in range(world)] for _ in range(nframes)]
 
     def one_step(events=None):
         with torch.cuda.stream(stream):
@@ -156,9 +157,7 @@ def main():
                     events[f][1].record(stream)
             if world > 1 and not args.no_gather:
                 for f in range(nframes):
-                    o = outs[f]
-                    flat = torch.cat([o["pos_steps"].view(-1), o["t"].view(torch.int32), o["info"]])
-                    dist.gather(flat, gather_bufs[f] if rank == 0 else None, dst=0)
+                    shard.gather_to_root(flats[f], rank, world, gather_bufs[f] if rank == 0 else None)
 
     for _ in range(args.warmup):
         one_step()
