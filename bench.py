@@ -105,6 +105,8 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cols", type=int, default=COLS)
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
+    ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -115,11 +117,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = local
+    dev = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     t0 = time.time()
     tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
@@ -157,7 +161,10 @@ def main():
                     events[f][1].record(stream)
             if world > 1 and not args.no_gather:
                 for f in range(nframes):
-                    shard.gather_to_root(flats[f], rank, world, gather_bufs[f] if rank == 0 else None)
+                    if args.dist_backend == "nccl":
+                        shard.gather_to_root(flats[f], rank, world, gather_bufs[f] if rank == 0 else None)
+                    else:  # gloo rehearsal: host copies
+                        shard.gather_to_root(flats[f].cpu(), rank, world, [b.cpu() for b in gather_bufs[f]] if rank == 0 else None)
 
     for _ in range(args.warmup):
         one_step()
@@ -184,6 +191,17 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     rays_per_launch = rt.Tree.count(descs[0])
 
+    if args.stats and rank == 0:
+        st = torch.zeros(8, dtype=torch.int64, device=dev)
+        d0 = descs[0]
+        d0.flags |= rt.CAST_STATS
+        d0.stats = st.data_ptr()
+        tree.cast(d0, outs[0], stream)
+        torch.cuda.synchronize()
+        d0.flags &= ~rt.CAST_STATS
+        vals = st.cpu().numpy()
+        print("stats per ray: " + ", ".join("%s=%.3f" % (k, v / max(1, vals[0])) for k, v in zip(rt.STAT_NAMES, vals) if k != "reserved"),
+              file=sys.stderr)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

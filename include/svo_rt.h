@@ -145,11 +145,16 @@ typedef struct {
     int32_t n_rays;
     int32_t steps;     /* DDA step budget per ray (castRayFromCam's `steps`) */
     int32_t flags;     /* SVO_CAST_* bits, 0 = default */
+    uint64_t* stats;   /* optional device u64[8] accumulating per-launch counters when
+                          flags & SVO_CAST_STATS: rays, lookups, node loads, cell skips,
+                          skips that ran out of budget, brick voxel steps, plain voxel steps */
 } svo_cast_desc;
 
 /* svo_cast_desc.flags: take every DDA step one at a time (disables the exact closed-form crossing
    of empty regions; results are identical — for testing and A/B timing) */
 #define SVO_CAST_ITERATIVE 1
+/* svo_cast_desc.flags: accumulate traversal counters into svo_cast_desc.stats (diagnostics) */
+#define SVO_CAST_STATS 2
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

@@ -32,6 +32,8 @@ MAT_MASK = 0xFFFF
 # Block flags (src/globals.hpp:68-74)
 NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
 CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B reference path)
+CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.stats
+STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "reserved")
 
 
 class SvoError(RuntimeError):
@@ -84,6 +86,7 @@ class CastDesc(C.Structure):
         ("n_rays", C.c_int32),
         ("steps", C.c_int32),
         ("flags", C.c_int32),
+        ("stats", C.c_void_p),
     ]
 
 

@@ -47,6 +47,7 @@ struct CastParams {
     int32_t mode;
     int32_t steps;
     int32_t flags;
+    unsigned long long* stats;
     // frame mode
     RayGen rg;
     float org[3];
@@ -218,11 +219,18 @@ __device__ __forceinline__ bool skip_cell(Ray& R, uint32_t wx, uint32_t wy, uint
 // breadth-first layout.
 enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
 
+struct Stats {
+    uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
+};
+
+template <bool STATS>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, uint32_t wx, uint32_t wy, uint32_t wz, uint32_t& sh_out,
-                                           uint64_t& bmask, uint32_t& bref, uint32_t& binfo) {
+                                           uint64_t& bmask, uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
+    if (STATS) st.lookups++;
     for (int32_t dd = 0; dd < P.levels; dd++) {
         const Node n = P.nodes[ni];
+        if (STATS) st.loads++;
         const uint32_t kind = n.info & K_KIND_MASK;
         if (kind == K_SOLID) {
             binfo = n.info;
@@ -252,6 +260,7 @@ __device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t
 }
 
 // One ray with castRayFromCam semantics.
+template <bool STATS>
 __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], const float d[3]) {
     Ray R;
     {
@@ -280,6 +289,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
+    Stats st = {0, 0, 0, 0, 0, 0};
     if (R.steps > 0) {
         dda_step(R);
         for (;;) {
@@ -287,7 +297,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
             uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
             uint32_t sh = 0u, bref = 0u, binfo = 0u;
             uint64_t bmask = 0ull;
-            const uint32_t kind = lookup(P, wx, wy, wz, sh, bmask, bref, binfo);
+            const uint32_t kind = lookup<STATS>(P, wx, wy, wz, sh, bmask, bref, binfo, st);
             if (kind == R_SOLID) {
                 hit = true;
                 mat = binfo >> 16;
@@ -306,6 +316,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
                     }
                     if (R.steps <= 0) break;
                     dda_step(R);
+                    if (STATS) st.brick_steps++;
                     wx = (uint32_t)R.rx & wm;
                     wy = (uint32_t)R.ry & wm;
                     wz = (uint32_t)R.rz & wm;
@@ -319,12 +330,19 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
             }
             // empty cell of size 2^sh around the voxel
             if (R.steps <= 0) break;
-            if (fast && skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) continue;
+            if (fast) {
+                if (skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
+                    if (STATS) st.skips++;
+                    continue;
+                }
+                if (STATS) st.skip_out++;
+            }
             // step through the cell without lookups (budget ends inside it, or not exact)
             const uint32_t cwx = wx, cwy = wy, cwz = wz;
             bool left = false;
             while (R.steps > 0) {
                 dda_step(R);
+                if (STATS) st.plain_steps++;
                 wx = (uint32_t)R.rx & wm;
                 wy = (uint32_t)R.ry & wm;
                 wz = (uint32_t)R.rz & wm;
@@ -335,6 +353,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
             }
             if (!left) break;
         }
+    }
+    if (STATS) {
+        atomicAdd(P.stats + 0, 1ull);
+        atomicAdd(P.stats + 1, (unsigned long long)st.lookups);
+        atomicAdd(P.stats + 2, (unsigned long long)st.loads);
+        atomicAdd(P.stats + 3, (unsigned long long)st.skips);
+        atomicAdd(P.stats + 4, (unsigned long long)st.skip_out);
+        atomicAdd(P.stats + 5, (unsigned long long)st.brick_steps);
+        atomicAdd(P.stats + 6, (unsigned long long)st.plain_steps);
     }
     Hit h;
     h.x = R.rx;
@@ -350,6 +377,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
     return h;
 }
 
+template <bool STATS>
 __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
     const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     float o[3], d[3];
@@ -392,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         }
         out = 0;
     }
-    const Hit h = trace(P, o, d);
+    const Hit h = trace<STATS>(P, o, d);
     reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
     P.t[out] = h.t;
     P.info[out] = h.info;
@@ -406,6 +434,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.steps = d->steps;
     P.flags = d->flags;
+    P.stats = reinterpret_cast<unsigned long long*>(d->stats);
     P.org[0] = d->origin[0];
     P.org[1] = d->origin[1];
     P.org[2] = d->origin[2];
@@ -489,6 +518,7 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (!o->pos_steps || !o->t || !o->info) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL output buffer");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_rays: tree not uploaded (svo_upload)");
     if (d->steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative step budget");
+    if ((d->flags & SVO_CAST_STATS) && !d->stats) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: SVO_CAST_STATS without a stats buffer");
     if (d->ray_dirs) {
         if (d->n_rays < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative ray count");
     } else if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0) {
@@ -502,7 +532,10 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
-    hipLaunchKernelGGL(k_cast, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    if (P.flags & SVO_CAST_STATS)
+        hipLaunchKernelGGL(k_cast<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    else
+        hipLaunchKernelGGL(k_cast<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -530,7 +563,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL(k_cast, dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL(k_cast<false>, dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
