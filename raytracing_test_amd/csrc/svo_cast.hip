@@ -48,6 +48,7 @@ struct CastParams {
     int32_t steps;
     int32_t flags;
     unsigned long long* stats;
+    uint32_t lds_nodes;
     // frame mode
     RayGen rg;
     float org[3];
@@ -64,6 +65,7 @@ struct CastParams {
 };
 
 constexpr int kBlock = 256;
+constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -223,14 +225,37 @@ struct Stats {
     uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
 };
 
+// The interior node whose child region holds the ray's current cell, kept in registers: a move to
+// a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
+// the descent at most one level down; leaving the parent's region restarts at the root, whose top
+// levels are staged in LDS.
+struct Parent {
+    uint64_t mask;
+    uint32_t ref;
+    uint32_t sh;  // child shift: a child region is 2^sh voxels wide, the parent's 2^(sh+2)
+    uint32_t wx, wy, wz;
+    bool valid;
+};
+
 template <bool STATS>
-__device__ __forceinline__ uint32_t lookup(const CastParams& P, uint32_t wx, uint32_t wy, uint32_t wz, uint32_t& sh_out,
-                                           uint64_t& bmask, uint32_t& bref, uint32_t& binfo, Stats& st) {
+__device__ __forceinline__ uint32_t lookup(const CastParams& P, const Node* __restrict__ lds, uint32_t nlds, uint32_t wx,
+                                           uint32_t wy, uint32_t wz, Parent& par, uint32_t& sh_out, uint64_t& bmask,
+                                           uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
+    int32_t dd = 0;
     if (STATS) st.lookups++;
-    for (int32_t dd = 0; dd < P.levels; dd++) {
-        const Node n = P.nodes[ni];
-        if (STATS) st.loads++;
+    if (par.valid && ((((wx ^ par.wx) | (wy ^ par.wy) | (wz ^ par.wz)) >> (par.sh + 2u)) == 0u)) {
+        const uint32_t sl = child_slot(wx, wy, wz, par.sh);
+        if (!((par.mask >> sl) & 1ull)) {
+            sh_out = par.sh;
+            return R_EMPTY;
+        }
+        ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
+        dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
+    }
+    for (; dd < P.levels; dd++) {
+        const Node n = ni < nlds ? lds[ni] : P.nodes[ni];
+        if (STATS) st.loads += ni < nlds ? 0u : 1u;
         const uint32_t kind = n.info & K_KIND_MASK;
         if (kind == K_SOLID) {
             binfo = n.info;
@@ -244,6 +269,13 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, uint32_t wx, uin
             return R_BRICK;
         }
         const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
+        par.mask = n.mask;
+        par.ref = n.ref;
+        par.sh = sh;
+        par.wx = wx;
+        par.wy = wy;
+        par.wz = wz;
+        par.valid = true;
         const uint32_t sl = child_slot(wx, wy, wz, sh);
         if (!((n.mask >> sl) & 1ull)) {
             sh_out = sh;
@@ -261,7 +293,8 @@ __device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t
 
 // One ray with castRayFromCam semantics.
 template <bool STATS>
-__device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], const float d[3]) {
+__device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict__ lds, uint32_t nlds, const float o[3],
+                                     const float d[3]) {
     Ray R;
     {
         const Dda1 ax = dda_axis(o[0], d[0]);
@@ -290,6 +323,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
     Stats st = {0, 0, 0, 0, 0, 0};
+    Parent par;
+    par.valid = false;
+    par.mask = 0ull;
+    par.ref = par.sh = par.wx = par.wy = par.wz = 0u;
     if (R.steps > 0) {
         dda_step(R);
         for (;;) {
@@ -297,7 +334,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
             uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
             uint32_t sh = 0u, bref = 0u, binfo = 0u;
             uint64_t bmask = 0ull;
-            const uint32_t kind = lookup<STATS>(P, wx, wy, wz, sh, bmask, bref, binfo, st);
+            const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
             if (kind == R_SOLID) {
                 hit = true;
                 mat = binfo >> 16;
@@ -379,6 +416,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const float o[3], cons
 
 template <bool STATS>
 __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
+    // top of the breadth-first array (root + the first levels) staged in LDS
+    __shared__ Node lds[kLdsNodes];
+    const uint32_t nlds = P.lds_nodes;
+    for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
+    __syncthreads();
     const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     float o[3], d[3];
     int64_t out;
@@ -420,7 +462,7 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         }
         out = 0;
     }
-    const Hit h = trace<STATS>(P, o, d);
+    const Hit h = trace<STATS>(P, lds, nlds, o, d);
     reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
     P.t[out] = h.t;
     P.info[out] = h.info;
@@ -435,6 +477,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.steps = d->steps;
     P.flags = d->flags;
     P.stats = reinterpret_cast<unsigned long long*>(d->stats);
+    P.lds_nodes = t->lds_nodes;
     P.org[0] = d->origin[0];
     P.org[1] = d->origin[1];
     P.org[2] = d->origin[2];
@@ -505,6 +548,13 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
     t->device = device;
     t->device_bytes = nb + mb + wb;
+    // stage whole levels from the top while they fit kLdsNodes
+    uint64_t acc = 0;
+    for (int lv = 0; lv < t->levels && lv < 8; lv++) {
+        if (acc + t->nodes_per_level[lv] > kLdsNodes) break;
+        acc += t->nodes_per_level[lv];
+    }
+    t->lds_nodes = (uint32_t)std::min<uint64_t>(acc, t->nodes.size());
     t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
     t->work_next = 0;
     return SVO_OK;
@@ -556,6 +606,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.mode = MODE_SINGLE;
     P.steps = steps;
+    P.lds_nodes = t->lds_nodes;
     for (int a = 0; a < 3; a++) {
         P.org[a] = pos[a];
         P.sdir[a] = dir[a];
