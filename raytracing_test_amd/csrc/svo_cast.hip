@@ -105,20 +105,21 @@ __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
     return dbl_ilogb(bound) + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
 }
 
-// #{ j >= 0 : T + j*a < V }  and  #{ j >= 0 : T + j*a <= V }   (exact under exact_axis)
+// #{ j >= 0 : T + j*a < V }  and  #{ j >= 0 : T + j*a <= V }, exact under exact_axis.  q = (V-T)/a
+// is estimated to within 1 (relative error ~2^-51), k0 = floor(q), and the exact remainder
+// r0 = V - (T + k0*a) (both terms on the ray's 2^lsb grid, below 2^(lsb+53)) picks k0, k0+1 or k0+2.
+// A count above the budget may be off, but then the skip is rejected anyway (total > steps).
 __device__ __forceinline__ int32_t count_lt(double T, double a, double inva, double V) {
     if (!(T < V)) return 0;
-    int32_t k = max(1, (int32_t)__builtin_ceil((V - T) * inva));
-    while (T + (double)k * a < V) k++;
-    while (k > 1 && T + (double)(k - 1) * a >= V) k--;
-    return k;
+    const int32_t k0 = (int32_t)((V - T) * inva);
+    const double r0 = V - (T + (double)k0 * a);
+    return k0 + (r0 > 0.0 ? 1 : 0) + (r0 > a ? 1 : 0);
 }
 __device__ __forceinline__ int32_t count_le(double T, double a, double inva, double V) {
     if (T > V) return 0;
-    int32_t k = max(1, (int32_t)__builtin_floor((V - T) * inva) + 1);
-    while (T + (double)k * a <= V) k++;
-    while (k > 1 && T + (double)(k - 1) * a > V) k--;
-    return k;
+    const int32_t k0 = (int32_t)((V - T) * inva);
+    const double r0 = V - (T + (double)k0 * a);
+    return k0 + (r0 >= 0.0 ? 1 : 0) + (r0 >= a ? 1 : 0);
 }
 
 struct Ray {
@@ -327,55 +328,66 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
     par.valid = false;
     par.mask = 0ull;
     par.ref = par.sh = par.wx = par.wy = par.wz = 0u;
+    // one action per iteration and lane (keeps the 64 lanes of a tile in step): a lookup of the voxel
+    // just entered (+ an O(1) crossing when it lies in an empty cell), or one voxel step in a brick
+    enum : uint32_t { M_LOOKUP = 0u, M_BRICK = 1u, M_DONE = 2u };
+    uint32_t mode = M_DONE;
     if (R.steps > 0) {
         dda_step(R);
-        for (;;) {
-            // the voxel just entered is untested
-            uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
-            uint32_t sh = 0u, bref = 0u, binfo = 0u;
-            uint64_t bmask = 0ull;
-            const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
-            if (kind == R_SOLID) {
-                hit = true;
-                mat = binfo >> 16;
-                break;
-            }
-            if (kind == R_BRICK) {
-                // voxel steps inside the brick, solid mask in registers
-                const uint32_t cwx = wx, cwy = wy, cwz = wz;
-                bool left = false;
-                for (;;) {
-                    const uint32_t v = child_slot(wx, wy, wz, 0u);
-                    if ((bmask >> v) & 1ull) {
-                        hit = true;
-                        mat = brick_material(P, bmask, bref, binfo, v);
-                        break;
-                    }
-                    if (R.steps <= 0) break;
-                    dda_step(R);
-                    if (STATS) st.brick_steps++;
-                    wx = (uint32_t)R.rx & wm;
-                    wy = (uint32_t)R.ry & wm;
-                    wz = (uint32_t)R.rz & wm;
-                    if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
-                        left = true;
-                        break;
-                    }
-                }
-                if (hit || !left) break;
+        mode = M_LOOKUP;
+    }
+    uint64_t bmask = 0ull;
+    uint32_t bref = 0u, binfo = 0u, cwx = 0u, cwy = 0u, cwz = 0u;
+    while (mode != M_DONE) {
+        uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
+        if (mode == M_BRICK) {
+            // one voxel step inside the brick, solid mask in registers
+            dda_step(R);
+            if (STATS) st.brick_steps++;
+            wx = (uint32_t)R.rx & wm;
+            wy = (uint32_t)R.ry & wm;
+            wz = (uint32_t)R.rz & wm;
+            if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
+                mode = M_LOOKUP;
                 continue;
             }
-            // empty cell of size 2^sh around the voxel
-            if (R.steps <= 0) break;
-            if (fast) {
-                if (skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
-                    if (STATS) st.skips++;
-                    continue;
-                }
-                if (STATS) st.skip_out++;
+            const uint32_t v = child_slot(wx, wy, wz, 0u);
+            if ((bmask >> v) & 1ull) {
+                hit = true;
+                mat = brick_material(P, bmask, bref, binfo, v);
+                mode = M_DONE;
+            } else if (R.steps <= 0) {
+                mode = M_DONE;
             }
-            // step through the cell without lookups (budget ends inside it, or not exact)
-            const uint32_t cwx = wx, cwy = wy, cwz = wz;
+            continue;
+        }
+        // M_LOOKUP: the voxel just entered is untested
+        uint32_t sh = 0u;
+        const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
+        if (kind == R_SOLID) {
+            hit = true;
+            mat = binfo >> 16;
+            mode = M_DONE;
+        } else if (kind == R_BRICK) {
+            cwx = wx;
+            cwy = wy;
+            cwz = wz;
+            const uint32_t v = child_slot(wx, wy, wz, 0u);
+            if ((bmask >> v) & 1ull) {
+                hit = true;
+                mat = brick_material(P, bmask, bref, binfo, v);
+                mode = M_DONE;
+            } else {
+                mode = R.steps > 0 ? M_BRICK : M_DONE;
+            }
+        } else if (R.steps <= 0) {
+            mode = M_DONE;
+        } else if (fast && skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
+            if (STATS) st.skips++;  // still M_LOOKUP: the exit voxel is untested
+        } else {
+            // budget ends inside the cell, or a non-exact ray: step through it without lookups
+            if (STATS && fast) st.skip_out++;
+            const uint32_t ewx = wx, ewy = wy, ewz = wz;
             bool left = false;
             while (R.steps > 0) {
                 dda_step(R);
@@ -383,12 +395,12 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
                 wx = (uint32_t)R.rx & wm;
                 wy = (uint32_t)R.ry & wm;
                 wz = (uint32_t)R.rz & wm;
-                if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> sh) != 0u) {
+                if ((((wx ^ ewx) | (wy ^ ewy) | (wz ^ ewz)) >> sh) != 0u) {
                     left = true;
                     break;
                 }
             }
-            if (!left) break;
+            mode = left ? M_LOOKUP : M_DONE;
         }
     }
     if (STATS) {
