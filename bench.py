@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--cols", type=int, default=COLS)
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
+    ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     args = ap.parse_args()
 
@@ -141,7 +142,7 @@ def main():
     n_pad = shard.max_shard_count(W, H, world)
     for f in range(nframes):
         d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
-                               flags=rt.CAST_ITERATIVE if args.iterative else 0)
+                               flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags)
         descs.append(d)
         flat, views = shard.alloc_flat(n_pad, torch.device("cuda", dev))
         flats.append(flat)

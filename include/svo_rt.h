@@ -155,6 +155,10 @@ typedef struct {
 #define SVO_CAST_ITERATIVE 1
 /* svo_cast_desc.flags: accumulate traversal counters into svo_cast_desc.stats (diagnostics) */
 #define SVO_CAST_STATS 2
+/* svo_cast_desc.flags, scheduling experiments (results identical): dispatch the frame's top tile
+   rows first / use the one-action-per-iteration traversal loop */
+#define SVO_CAST_TOP_FIRST 4
+#define SVO_CAST_FLAT 8
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

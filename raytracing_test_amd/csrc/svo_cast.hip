@@ -293,7 +293,7 @@ __device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t
 }
 
 // One ray with castRayFromCam semantics.
-template <bool STATS>
+template <bool STATS, bool FLAT>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict__ lds, uint32_t nlds, const float o[3],
                                      const float d[3]) {
     Ray R;
@@ -328,6 +328,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
     par.valid = false;
     par.mask = 0ull;
     par.ref = par.sh = par.wx = par.wy = par.wz = 0u;
+    if (FLAT) {
     // one action per iteration and lane (keeps the 64 lanes of a tile in step): a lookup of the voxel
     // just entered (+ an O(1) crossing when it lies in an empty cell), or one voxel step in a brick
     enum : uint32_t { M_LOOKUP = 0u, M_BRICK = 1u, M_DONE = 2u };
@@ -403,6 +404,72 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
             mode = left ? M_LOOKUP : M_DONE;
         }
     }
+    } else {
+    if (R.steps > 0) {
+        dda_step(R);
+        for (;;) {
+            // the voxel just entered is untested
+            uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
+            uint32_t sh = 0u, bref = 0u, binfo = 0u;
+            uint64_t bmask = 0ull;
+            const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
+            if (kind == R_SOLID) {
+                hit = true;
+                mat = binfo >> 16;
+                break;
+            }
+            if (kind == R_BRICK) {
+                // voxel steps inside the brick, solid mask in registers
+                const uint32_t cwx = wx, cwy = wy, cwz = wz;
+                bool left = false;
+                for (;;) {
+                    const uint32_t v = child_slot(wx, wy, wz, 0u);
+                    if ((bmask >> v) & 1ull) {
+                        hit = true;
+                        mat = brick_material(P, bmask, bref, binfo, v);
+                        break;
+                    }
+                    if (R.steps <= 0) break;
+                    dda_step(R);
+                    if (STATS) st.brick_steps++;
+                    wx = (uint32_t)R.rx & wm;
+                    wy = (uint32_t)R.ry & wm;
+                    wz = (uint32_t)R.rz & wm;
+                    if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
+                        left = true;
+                        break;
+                    }
+                }
+                if (hit || !left) break;
+                continue;
+            }
+            // empty cell of size 2^sh around the voxel
+            if (R.steps <= 0) break;
+            if (fast) {
+                if (skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
+                    if (STATS) st.skips++;
+                    continue;
+                }
+                if (STATS) st.skip_out++;
+            }
+            // step through the cell without lookups (budget ends inside it, or not exact)
+            const uint32_t ewx = wx, ewy = wy, ewz = wz;
+            bool left = false;
+            while (R.steps > 0) {
+                dda_step(R);
+                if (STATS) st.plain_steps++;
+                wx = (uint32_t)R.rx & wm;
+                wy = (uint32_t)R.ry & wm;
+                wz = (uint32_t)R.rz & wm;
+                if ((((wx ^ ewx) | (wy ^ ewy) | (wz ^ ewz)) >> sh) != 0u) {
+                    left = true;
+                    break;
+                }
+            }
+            if (!left) break;
+        }
+    }
+    }
     if (STATS) {
         atomicAdd(P.stats + 0, 1ull);
         atomicAdd(P.stats + 1, (unsigned long long)st.lookups);
@@ -426,7 +493,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
     return h;
 }
 
-template <bool STATS>
+template <bool STATS, bool FLAT>
 __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
     // top of the breadth-first array (root + the first levels) staged in LDS
     __shared__ Node lds[kLdsNodes];
@@ -440,9 +507,10 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes
         const int64_t tile = g >> 6;
         const int32_t lane = (int32_t)(g & 63);
-        const int32_t trl = (int32_t)(tile / P.tiles_x);
+        int32_t trl = (int32_t)(tile / P.tiles_x);
+        if (P.flags & SVO_CAST_TOP_FIRST) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - (int64_t)trl * P.tiles_x);
-        if (trl >= P.tile_rows_local) return;
+        if (trl < 0 || trl >= P.tile_rows_local) return;
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         const int32_t px = tx * 8 + (lane & 7), py = tr * 8 + (lane >> 3);
         if (px >= P.width || py >= P.height) return;
@@ -474,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         }
         out = 0;
     }
-    const Hit h = trace<STATS>(P, lds, nlds, o, d);
+    const Hit h = trace<STATS, FLAT>(P, lds, nlds, o, d);
     reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
     P.t[out] = h.t;
     P.info[out] = h.info;
@@ -594,10 +662,14 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
-    if (P.flags & SVO_CAST_STATS)
-        hipLaunchKernelGGL(k_cast<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-    else
-        hipLaunchKernelGGL(k_cast<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    const bool flat = (P.flags & SVO_CAST_FLAT) != 0;
+    if (P.flags & SVO_CAST_STATS) {
+        if (flat) hipLaunchKernelGGL((k_cast<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+        else hipLaunchKernelGGL((k_cast<true, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    } else {
+        if (flat) hipLaunchKernelGGL((k_cast<false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+        else hipLaunchKernelGGL((k_cast<false, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -626,7 +698,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL(k_cast<false>, dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL((k_cast<false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
