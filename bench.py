@@ -193,7 +193,7 @@ def main():
     rays_per_launch = rt.Tree.count(descs[0])
 
     if args.stats and rank == 0:
-        st = torch.zeros(8, dtype=torch.int64, device=dev)
+        st = torch.zeros(16, dtype=torch.int64, device=dev)
         d0 = descs[0]
         d0.flags |= rt.CAST_STATS
         d0.stats = st.data_ptr()
@@ -201,8 +201,8 @@ def main():
         torch.cuda.synchronize()
         d0.flags &= ~rt.CAST_STATS
         vals = st.cpu().numpy()
-        print("stats per ray: " + ", ".join("%s=%.3f" % (k, v / max(1, vals[0])) for k, v in zip(rt.STAT_NAMES, vals) if k != "reserved"),
-              file=sys.stderr)
+        print("stats per ray: " + ", ".join("%s=%.3f" % (k, v / max(1, vals[0])) for k, v in zip(rt.STAT_NAMES, vals)) +
+              "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

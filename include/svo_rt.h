@@ -145,9 +145,10 @@ typedef struct {
     int32_t n_rays;
     int32_t steps;     /* DDA step budget per ray (castRayFromCam's `steps`) */
     int32_t flags;     /* SVO_CAST_* bits, 0 = default */
-    uint64_t* stats;   /* optional device u64[8] accumulating per-launch counters when
+    uint64_t* stats;   /* optional device u64[16] accumulating per-launch counters when
                           flags & SVO_CAST_STATS: rays, lookups, node loads, cell skips,
-                          skips that ran out of budget, brick voxel steps, plain voxel steps */
+                          skips that ran out of budget, brick voxel steps, plain voxel steps,
+                          lane work units, wave-max work units x 64 */
 } svo_cast_desc;
 
 /* svo_cast_desc.flags: take every DDA step one at a time (disables the exact closed-form crossing
@@ -159,6 +160,8 @@ typedef struct {
    rows first / use the one-action-per-iteration traversal loop */
 #define SVO_CAST_TOP_FIRST 4
 #define SVO_CAST_FLAT 8
+/* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
+#define SVO_CAST_XCD_SWIZZLE 16
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

@@ -226,6 +226,16 @@ struct Stats {
     uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
 };
 
+// wave-wide max / sum (diagnostics only)
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
+
 // The interior node whose child region holds the ray's current cell, kept in registers: a move to
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
 // the descent at most one level down; leaving the parent's region restarts at the root, whose top
@@ -471,6 +481,13 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
     }
     }
     if (STATS) {
+        // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
+        const uint32_t work = st.lookups + st.brick_steps + st.plain_steps;
+        const uint32_t wmax = wave_max(work), wsum = wave_sum(work);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(P.stats + 7, (unsigned long long)wsum);
+            atomicAdd(P.stats + 8, (unsigned long long)wmax * 64ull);
+        }
         atomicAdd(P.stats + 0, 1ull);
         atomicAdd(P.stats + 1, (unsigned long long)st.lookups);
         atomicAdd(P.stats + 2, (unsigned long long)st.loads);
@@ -500,7 +517,15 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
     const uint32_t nlds = P.lds_nodes;
     for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
     __syncthreads();
-    const int64_t g = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    int64_t blk = blockIdx.x;
+    if (P.flags & SVO_CAST_XCD_SWIZZLE) {
+        // blocks are dealt round-robin to the 8 XCDs (blk % 8 share an L2): give each XCD one
+        // contiguous band of tiles so neighbouring tiles hit the same L2
+        const int64_t nb = gridDim.x, per = (nb + 7) / 8, x = blk & 7, k = blk >> 3;
+        const int64_t full = nb - (per - 1) * 8;  // XCDs 0..full-1 receive `per` blocks
+        blk = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+    }
+    const int64_t g = blk * kBlock + threadIdx.x;
     float o[3], d[3];
     int64_t out;
     if (P.mode == MODE_FRAME) {
