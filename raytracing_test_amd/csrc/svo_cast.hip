@@ -512,6 +512,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
 
 template <bool STATS, bool FLAT>
 __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
+    // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
+    unsigned long long t_start = 0;
+    if (STATS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     // top of the breadth-first array (root + the first levels) staged in LDS
     __shared__ Node lds[kLdsNodes];
     const uint32_t nlds = P.lds_nodes;
@@ -526,51 +529,61 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         blk = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
     }
     const int64_t g = blk * kBlock + threadIdx.x;
-    float o[3], d[3];
-    int64_t out;
+    float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
+    int64_t out = -1;
     if (P.mode == MODE_FRAME) {
         // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes
         const int64_t tile = g >> 6;
         const int32_t lane = (int32_t)(g & 63);
         int32_t trl = (int32_t)(tile / P.tiles_x);
         if (P.flags & SVO_CAST_TOP_FIRST) trl = P.tile_rows_local - 1 - trl;
-        const int32_t tx = (int32_t)(tile - (int64_t)trl * P.tiles_x);
-        if (trl < 0 || trl >= P.tile_rows_local) return;
+        const int32_t tx = (int32_t)(tile - (int64_t)(tile / P.tiles_x) * P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         const int32_t px = tx * 8 + (lane & 7), py = tr * 8 + (lane >> 3);
-        if (px >= P.width || py >= P.height) return;
-        raygen_pixel(P.rg, px, py, d);
-        o[0] = P.org[0];
-        o[1] = P.org[1];
-        o[2] = P.org[2];
-        out = ((int64_t)trl * 8 + (lane >> 3)) * P.width + px;
-    } else if (P.mode == MODE_EXPLICIT) {
-        if (g >= P.n_rays) return;
-        d[0] = P.rdir[3 * g + 0];
-        d[1] = P.rdir[3 * g + 1];
-        d[2] = P.rdir[3 * g + 2];
-        if (P.rorg) {
-            o[0] = P.rorg[3 * g + 0];
-            o[1] = P.rorg[3 * g + 1];
-            o[2] = P.rorg[3 * g + 2];
-        } else {
+        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+            raygen_pixel(P.rg, px, py, d);
             o[0] = P.org[0];
             o[1] = P.org[1];
             o[2] = P.org[2];
+            out = ((int64_t)trl * 8 + (lane >> 3)) * P.width + px;
         }
-        out = g;
-    } else {
-        if (g != 0) return;
+    } else if (P.mode == MODE_EXPLICIT) {
+        if (g < P.n_rays) {
+            d[0] = P.rdir[3 * g + 0];
+            d[1] = P.rdir[3 * g + 1];
+            d[2] = P.rdir[3 * g + 2];
+            if (P.rorg) {
+                o[0] = P.rorg[3 * g + 0];
+                o[1] = P.rorg[3 * g + 1];
+                o[2] = P.rorg[3 * g + 2];
+            } else {
+                o[0] = P.org[0];
+                o[1] = P.org[1];
+                o[2] = P.org[2];
+            }
+            out = g;
+        }
+    } else if (g == 0) {
         for (int a = 0; a < 3; a++) {
             d[a] = P.sdir[a];
             o[a] = P.org[a];
         }
         out = 0;
     }
-    const Hit h = trace<STATS, FLAT>(P, lds, nlds, o, d);
-    reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
-    P.t[out] = h.t;
-    P.info[out] = h.info;
+    if (out >= 0) {
+        const Hit h = trace<STATS, FLAT>(P, lds, nlds, o, d);
+        reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
+        P.t[out] = h.t;
+        P.info[out] = h.info;
+    }
+    if (STATS) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+            P.stats[16 + 2 * blockIdx.x] = t_start;
+            P.stats[16 + 2 * blockIdx.x + 1] = t_end;
+        }
+    }
 }
 
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
