@@ -34,7 +34,7 @@ def per_dispatch(d, kernel="k_cast"):
 def main(out):
     res = {"kernel": "k_cast", "source": out}
     counters = {}
-    for d in sorted(glob.glob(os.path.join(out, "pmc_*"))):
+    for d in sorted(glob.glob(os.path.join(out, "pmc_*")) + glob.glob(os.path.join(out, "sq_*"))):
         if os.path.isdir(d):
             c, n = per_dispatch(d)
             counters.update(c)
