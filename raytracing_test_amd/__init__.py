@@ -34,7 +34,6 @@ NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
 CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B reference path)
 CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.stats
 CAST_TOP_FIRST = 4  # scheduling experiment: top tile rows first
-CAST_FLAT = 8  # scheduling experiment: one action per loop iteration
 CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64")

@@ -83,13 +83,13 @@ struct Hit {
 // directly equals the k-fold accumulation bit for bit.  Such a ray ("fast") crosses an empty
 // region in O(1): the first event to leave the region is the lexicographic minimum of the three
 // per-axis exit events, and the events before it on the other axes are counted by division
-// (with an exact +-1 fix-up).  Rays that fail the test step voxel by voxel (still without memory
+// (with an exact fix-up).  Rays that fail the test step voxel by voxel (still without memory
 // traffic inside known-empty regions).  Both paths give identical results (tests).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int dbl_lsb(double x) {
     const uint64_t b = (uint64_t)__double_as_longlong(x);
     const int ef = (int)((b >> 52) & 0x7FF);
-    uint64_t m = b & 0xFFFFFFFFFFFFFull;
+    const uint64_t m = b & 0xFFFFFFFFFFFFFull;
     if (ef == 0) return m ? -1074 + __builtin_ctzll(m) : (1 << 20);
     return ef - 1075 + __builtin_ctzll(m | (1ull << 52));
 }
@@ -105,53 +105,44 @@ __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
     return dbl_ilogb(bound) + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
 }
 
-// #{ j >= 0 : T + j*a < V }  and  #{ j >= 0 : T + j*a <= V }, exact under exact_axis.  q = (V-T)/a
-// is estimated to within 1 (relative error ~2^-51), k0 = floor(q), and the exact remainder
-// r0 = V - (T + k0*a) (both terms on the ray's 2^lsb grid, below 2^(lsb+53)) picks k0, k0+1 or k0+2.
-// A count above the budget may be off, but then the skip is rejected anyway (total > steps).
-__device__ __forceinline__ int32_t count_lt(double T, double a, double inva, double V) {
-    if (!(T < V)) return 0;
-    const int32_t k0 = (int32_t)((V - T) * inva);
+// Number of events j >= 0 of the sequence T + j*a that come before an event of value V on another
+// axis: those with T + j*a < V (strict: this axis loses ties) or <= V.  Exact under exact_axis:
+// q = (V-T)/a is estimated to within 1 (f32 reciprocal, relative error < 2^-22), k0 = trunc(q),
+// and the exact remainder r0 = V - (T + k0*a) (all terms on the ray's 2^lsb grid, below
+// 2^(lsb+53)) settles k0, k0+1 or k0+2.  Counts above the budget may be off; the caller then
+// rejects the move anyway (total > steps).  Branch-free.
+__device__ __forceinline__ int32_t count_before(double T, double a, float inva, double V, bool strict) {
+    const double q = (V - T) * (double)inva;
+    const int32_t k0 = q > 0.0 ? (int32_t)q : 0;
     const double r0 = V - (T + (double)k0 * a);
-    return k0 + (r0 > 0.0 ? 1 : 0) + (r0 > a ? 1 : 0);
-}
-__device__ __forceinline__ int32_t count_le(double T, double a, double inva, double V) {
-    if (T > V) return 0;
-    const int32_t k0 = (int32_t)((V - T) * inva);
-    const double r0 = V - (T + (double)k0 * a);
-    return k0 + (r0 >= 0.0 ? 1 : 0) + (r0 >= a ? 1 : 0);
+    const int32_t k = k0 + (strict ? (int32_t)(r0 > 0.0) + (int32_t)(r0 > a) : (int32_t)(r0 >= 0.0) + (int32_t)(r0 >= a));
+    return k;
 }
 
 struct Ray {
-    int32_t rx, ry, rz;
-    double tx, ty, tz;  // next crossing per axis (deltaPos)
-    double ax, ay, az;  // absDelta
-    int32_t sx, sy, sz;
-    int32_t steps;
-    uint32_t axis;
-    double tlast;
+    int32_t r[3];   // current voxel (unwrapped)
+    double T[3];    // next crossing per axis (deltaPos)
+    double a[3];    // absDelta
+    float ia[3];    // 1/absDelta estimate (counts only)
+    int32_t s[3];   // step
+    int32_t steps;  // budget left
+    uint32_t axis;  // axis of the last step (3: none)
+    double tlast;   // crossing value of the last step
 };
 
-// one DDA step (ray_caster.cpp:70-80)
+// one DDA step (ray_caster.cpp:70-80), branch-free
 __device__ __forceinline__ void dda_step(Ray& R) {
-    const bool cx = (R.tx < R.ty) && (R.tx < R.tz);
-    const bool cy = !cx && (R.ty < R.tz);
-    if (cx) {
-        R.rx += R.sx;
-        R.tlast = R.tx;
-        R.tx += R.ax;
-        R.axis = 0u;
-    } else if (cy) {
-        R.ry += R.sy;
-        R.tlast = R.ty;
-        R.ty += R.ay;
-        R.axis = 1u;
-    } else {
-        R.rz += R.sz;
-        R.tlast = R.tz;
-        R.tz += R.az;
-        R.axis = 2u;
-    }
+    const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+    const bool cy = !cx && (R.T[1] < R.T[2]);
+    const bool cz = !cx && !cy;
+    R.tlast = cx ? R.T[0] : (cy ? R.T[1] : R.T[2]);
+    R.axis = cx ? 0u : (cy ? 1u : 2u);
+    R.r[0] += cx ? R.s[0] : 0;
+    R.r[1] += cy ? R.s[1] : 0;
+    R.r[2] += cz ? R.s[2] : 0;
+    R.T[0] = cx ? R.T[0] + R.a[0] : R.T[0];
+    R.T[1] = cy ? R.T[1] + R.a[1] : R.T[1];
+    R.T[2] = cz ? R.T[2] + R.a[2] : R.T[2];
     R.steps--;
 }
 
@@ -161,66 +152,42 @@ __device__ __forceinline__ int32_t exit_steps(uint32_t w, int32_t s, uint32_t sh
     return s > 0 ? (int32_t)(lo + (1u << sh) - w) : (int32_t)(w - lo + 1u);
 }
 
-// Cross the empty aligned cell of size 2^sh containing the current voxel in one move.  Returns
-// false (state unchanged) when the budget ends inside the cell.
-__device__ __forceinline__ bool skip_cell(Ray& R, uint32_t wx, uint32_t wy, uint32_t wz, uint32_t sh, double iax, double iay,
-                                          double iaz) {
+// Cross the empty aligned cell of size 2^sh containing the current voxel in one move, branch-free
+// over the exit axis.  Returns false (state unchanged) when the budget ends inside the cell.
+__device__ __forceinline__ bool skip_cell(Ray& R, const uint32_t w[3], uint32_t sh) {
     const int32_t lim = R.steps + 1;  // exits beyond the budget are clamped (safe: total > steps)
-    const int32_t ex = min(exit_steps(wx, R.sx, sh), lim);
-    const int32_t ey = min(exit_steps(wy, R.sy, sh), lim);
-    const int32_t ez = min(exit_steps(wz, R.sz, sh), lim);
-    const double Ex = R.tx + (double)(ex - 1) * R.ax;
-    const double Ey = R.ty + (double)(ey - 1) * R.ay;
-    const double Ez = R.tz + (double)(ez - 1) * R.az;
-    int32_t cx, cy, cz, total;
-    if ((Ex < Ey) && (Ex < Ez)) {  // x leaves first; y, z events tied with it come before it
-        cy = count_le(R.ty, R.ay, iay, Ex);
-        cz = count_le(R.tz, R.az, iaz, Ex);
-        total = ex + cy + cz;
-        if (total > R.steps) return false;
-        R.rx += R.sx * ex;
-        R.ry += R.sy * cy;
-        R.rz += R.sz * cz;
-        R.ty += (double)cy * R.ay;
-        R.tz += (double)cz * R.az;
-        R.tlast = Ex;
-        R.tx = Ex + R.ax;
-        R.axis = 0u;
-    } else if (Ey < Ez) {  // y first; tied x events come after it, tied z events before
-        cx = count_lt(R.tx, R.ax, iax, Ey);
-        cz = count_le(R.tz, R.az, iaz, Ey);
-        total = ey + cx + cz;
-        if (total > R.steps) return false;
-        R.rx += R.sx * cx;
-        R.ry += R.sy * ey;
-        R.rz += R.sz * cz;
-        R.tx += (double)cx * R.ax;
-        R.tz += (double)cz * R.az;
-        R.tlast = Ey;
-        R.ty = Ey + R.ay;
-        R.axis = 1u;
-    } else {  // z first; tied x and y events come after it
-        cx = count_lt(R.tx, R.ax, iax, Ez);
-        cy = count_lt(R.ty, R.ay, iay, Ez);
-        total = ez + cx + cy;
-        if (total > R.steps) return false;
-        R.rx += R.sx * cx;
-        R.ry += R.sy * cy;
-        R.rz += R.sz * ez;
-        R.tx += (double)cx * R.ax;
-        R.ty += (double)cy * R.ay;
-        R.tlast = Ez;
-        R.tz = Ez + R.az;
-        R.axis = 2u;
+    int32_t e[3];
+    double E[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        e[k] = min(exit_steps(w[k], R.s[k], sh), lim);
+        E[k] = R.T[k] + (double)(e[k] - 1) * R.a[k];
     }
+    // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
+    const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
+    const bool by = !bx && (E[1] < E[2]);
+    const uint32_t b = bx ? 0u : (by ? 1u : 2u);
+    const double V = bx ? E[0] : (by ? E[1] : E[2]);
+    int32_t n[3];
+    int32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        // axis k's events tied with V come after the exit event when rank_k > rank_b (k < b)
+        const int32_t c = count_before(R.T[k], R.a[k], R.ia[k], V, (uint32_t)k < b);
+        n[k] = (uint32_t)k == b ? e[k] : c;
+        total += n[k];
+    }
+    if (total > R.steps) return false;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        R.r[k] += R.s[k] * n[k];
+        R.T[k] += (double)n[k] * R.a[k];
+    }
+    R.tlast = V;
+    R.axis = b;
     R.steps -= total;
     return true;
 }
-
-// Region lookup of a wrapped voxel: SOLID hit, an empty child cell (returns its shift), or the
-// brick holding the voxel (mask / ref / info returned).  tetrahexa_tree.cpp:124-152 on the
-// breadth-first layout.
-enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
 
 struct Stats {
     uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
@@ -236,6 +203,11 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+// Region lookup of a wrapped voxel: SOLID hit, an empty child cell (returns its shift), or the
+// brick holding the voxel (mask / ref / info returned).  tetrahexa_tree.cpp:124-152 on the
+// breadth-first layout.
+enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
+
 // The interior node whose child region holds the ray's current cell, kept in registers: a move to
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
 // the descent at most one level down; leaving the parent's region restarts at the root, whose top
@@ -244,19 +216,30 @@ struct Parent {
     uint64_t mask;
     uint32_t ref;
     uint32_t sh;  // child shift: a child region is 2^sh voxels wide, the parent's 2^(sh+2)
-    uint32_t wx, wy, wz;
+    uint32_t w[3];
     bool valid;
 };
 
+// global node read through a buffer resource (32-bit offsets, never merged with the LDS path)
+__device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uint32_t ni) {
+    const uint32_t off = ni << 4;
+    Node n;
+    n.mask = ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0) << 32);
+    n.ref = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 8, 0, 0);
+    n.info = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 12, 0, 0);
+    return n;
+}
+
 template <bool STATS>
-__device__ __forceinline__ uint32_t lookup(const CastParams& P, const Node* __restrict__ lds, uint32_t nlds, uint32_t wx,
-                                           uint32_t wy, uint32_t wz, Parent& par, uint32_t& sh_out, uint64_t& bmask,
+__device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
+                                           uint32_t nlds, const uint32_t w[3], Parent& par, uint32_t& sh_out, uint64_t& bmask,
                                            uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
-    if (par.valid && ((((wx ^ par.wx) | (wy ^ par.wy) | (wz ^ par.wz)) >> (par.sh + 2u)) == 0u)) {
-        const uint32_t sl = child_slot(wx, wy, wz, par.sh);
+    if (par.valid && ((((w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2])) >> (par.sh + 2u)) == 0u)) {
+        const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
         if (!((par.mask >> sl) & 1ull)) {
             sh_out = par.sh;
             return R_EMPTY;
@@ -265,29 +248,30 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Node* __re
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
     }
     for (; dd < P.levels; dd++) {
-        const Node n = ni < nlds ? lds[ni] : P.nodes[ni];
-        if (STATS) st.loads += ni < nlds ? 0u : 1u;
-        const uint32_t kind = n.info & K_KIND_MASK;
-        if (kind == K_SOLID) {
-            binfo = n.info;
-            return R_SOLID;
+        Node n;
+        if (ni < nlds) {
+            n = lds[ni];
+        } else {
+            n = load_node(rsrc, ni);
+            if (STATS) st.loads++;
         }
-        if (kind == K_BRICK) {
+        const uint32_t kind = n.info & K_KIND_MASK;
+        if (kind != K_INTERIOR) {
             bmask = n.mask;
             bref = n.ref;
             binfo = n.info;
             sh_out = 2u;
-            return R_BRICK;
+            return kind == K_SOLID ? R_SOLID : R_BRICK;
         }
         const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
         par.mask = n.mask;
         par.ref = n.ref;
         par.sh = sh;
-        par.wx = wx;
-        par.wy = wy;
-        par.wz = wz;
+        par.w[0] = w[0];
+        par.w[1] = w[1];
+        par.w[2] = w[2];
         par.valid = true;
-        const uint32_t sl = child_slot(wx, wy, wz, sh);
+        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
         if (!((n.mask >> sl) & 1ull)) {
             sh_out = sh;
             return R_EMPTY;
@@ -302,34 +286,35 @@ __device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t
     return (info & K_UNIFORM) ? (info >> 16) : (uint32_t)P.mats[ref + (uint32_t)__popcll(mask & ((1ull << v) - 1ull))];
 }
 
+__device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) {
+    w[0] = (uint32_t)R.r[0] & wm;
+    w[1] = (uint32_t)R.r[1] & wm;
+    w[2] = (uint32_t)R.r[2] & wm;
+}
+
+__device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[3], uint32_t sh) {
+    return (((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2])) >> sh) == 0u;
+}
+
 // One ray with castRayFromCam semantics.
-template <bool STATS, bool FLAT>
-__device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict__ lds, uint32_t nlds, const float o[3],
-                                     const float d[3]) {
+template <bool STATS>
+__device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
+                                     uint32_t nlds, const float o[3], const float d[3]) {
     Ray R;
-    {
-        const Dda1 ax = dda_axis(o[0], d[0]);
-        const Dda1 ay = dda_axis(o[1], d[1]);
-        const Dda1 az = dda_axis(o[2], d[2]);
-        R.rx = ax.cell;
-        R.ry = ay.cell;
-        R.rz = az.cell;
-        R.tx = ax.dpos;
-        R.ty = ay.dpos;
-        R.tz = az.dpos;
-        R.ax = ax.adelta;
-        R.ay = ay.adelta;
-        R.az = az.adelta;
-        R.sx = ax.step;
-        R.sy = ay.step;
-        R.sz = az.step;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const Dda1 ax = dda_axis(o[k], d[k]);
+        R.r[k] = ax.cell;
+        R.T[k] = ax.dpos;
+        R.a[k] = ax.adelta;
+        R.s[k] = ax.step;
+        R.ia[k] = (float)(1.0 / ax.adelta);
     }
     R.steps = P.steps;
     R.axis = 3u;
     R.tlast = 0.0;
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.tx, R.ax, P.steps) && exact_axis(R.ty, R.ay, P.steps) &&
-                      exact_axis(R.tz, R.az, P.steps);
-    const double iax = 1.0 / R.ax, iay = 1.0 / R.ay, iaz = 1.0 / R.az;
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a[0], P.steps) && exact_axis(R.T[1], R.a[1], P.steps) &&
+                      exact_axis(R.T[2], R.a[2], P.steps);
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -337,92 +322,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
     Parent par;
     par.valid = false;
     par.mask = 0ull;
-    par.ref = par.sh = par.wx = par.wy = par.wz = 0u;
-    if (FLAT) {
-    // one action per iteration and lane (keeps the 64 lanes of a tile in step): a lookup of the voxel
-    // just entered (+ an O(1) crossing when it lies in an empty cell), or one voxel step in a brick
-    enum : uint32_t { M_LOOKUP = 0u, M_BRICK = 1u, M_DONE = 2u };
-    uint32_t mode = M_DONE;
-    if (R.steps > 0) {
-        dda_step(R);
-        mode = M_LOOKUP;
-    }
-    uint64_t bmask = 0ull;
-    uint32_t bref = 0u, binfo = 0u, cwx = 0u, cwy = 0u, cwz = 0u;
-    while (mode != M_DONE) {
-        uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
-        if (mode == M_BRICK) {
-            // one voxel step inside the brick, solid mask in registers
-            dda_step(R);
-            if (STATS) st.brick_steps++;
-            wx = (uint32_t)R.rx & wm;
-            wy = (uint32_t)R.ry & wm;
-            wz = (uint32_t)R.rz & wm;
-            if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
-                mode = M_LOOKUP;
-                continue;
-            }
-            const uint32_t v = child_slot(wx, wy, wz, 0u);
-            if ((bmask >> v) & 1ull) {
-                hit = true;
-                mat = brick_material(P, bmask, bref, binfo, v);
-                mode = M_DONE;
-            } else if (R.steps <= 0) {
-                mode = M_DONE;
-            }
-            continue;
-        }
-        // M_LOOKUP: the voxel just entered is untested
-        uint32_t sh = 0u;
-        const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
-        if (kind == R_SOLID) {
-            hit = true;
-            mat = binfo >> 16;
-            mode = M_DONE;
-        } else if (kind == R_BRICK) {
-            cwx = wx;
-            cwy = wy;
-            cwz = wz;
-            const uint32_t v = child_slot(wx, wy, wz, 0u);
-            if ((bmask >> v) & 1ull) {
-                hit = true;
-                mat = brick_material(P, bmask, bref, binfo, v);
-                mode = M_DONE;
-            } else {
-                mode = R.steps > 0 ? M_BRICK : M_DONE;
-            }
-        } else if (R.steps <= 0) {
-            mode = M_DONE;
-        } else if (fast && skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
-            if (STATS) st.skips++;  // still M_LOOKUP: the exit voxel is untested
-        } else {
-            // budget ends inside the cell, or a non-exact ray: step through it without lookups
-            if (STATS && fast) st.skip_out++;
-            const uint32_t ewx = wx, ewy = wy, ewz = wz;
-            bool left = false;
-            while (R.steps > 0) {
-                dda_step(R);
-                if (STATS) st.plain_steps++;
-                wx = (uint32_t)R.rx & wm;
-                wy = (uint32_t)R.ry & wm;
-                wz = (uint32_t)R.rz & wm;
-                if ((((wx ^ ewx) | (wy ^ ewy) | (wz ^ ewz)) >> sh) != 0u) {
-                    left = true;
-                    break;
-                }
-            }
-            mode = left ? M_LOOKUP : M_DONE;
-        }
-    }
-    } else {
+    par.ref = par.sh = par.w[0] = par.w[1] = par.w[2] = 0u;
     if (R.steps > 0) {
         dda_step(R);
         for (;;) {
             // the voxel just entered is untested
-            uint32_t wx = (uint32_t)R.rx & wm, wy = (uint32_t)R.ry & wm, wz = (uint32_t)R.rz & wm;
+            uint32_t w[3];
+            wrap3(R, wm, w);
             uint32_t sh = 0u, bref = 0u, binfo = 0u;
             uint64_t bmask = 0ull;
-            const uint32_t kind = lookup<STATS>(P, lds, nlds, wx, wy, wz, par, sh, bmask, bref, binfo, st);
+            const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, w, par, sh, bmask, bref, binfo, st);
             if (kind == R_SOLID) {
                 hit = true;
                 mat = binfo >> 16;
@@ -430,10 +339,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
             }
             if (kind == R_BRICK) {
                 // voxel steps inside the brick, solid mask in registers
-                const uint32_t cwx = wx, cwy = wy, cwz = wz;
+                const uint32_t c[3] = {w[0], w[1], w[2]};
                 bool left = false;
                 for (;;) {
-                    const uint32_t v = child_slot(wx, wy, wz, 0u);
+                    const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
                     if ((bmask >> v) & 1ull) {
                         hit = true;
                         mat = brick_material(P, bmask, bref, binfo, v);
@@ -442,10 +351,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
                     if (R.steps <= 0) break;
                     dda_step(R);
                     if (STATS) st.brick_steps++;
-                    wx = (uint32_t)R.rx & wm;
-                    wy = (uint32_t)R.ry & wm;
-                    wz = (uint32_t)R.rz & wm;
-                    if ((((wx ^ cwx) | (wy ^ cwy) | (wz ^ cwz)) >> 2) != 0u) {
+                    wrap3(R, wm, w);
+                    if (!same_cell(w, c, 2u)) {
                         left = true;
                         break;
                     }
@@ -456,29 +363,26 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
             // empty cell of size 2^sh around the voxel
             if (R.steps <= 0) break;
             if (fast) {
-                if (skip_cell(R, wx, wy, wz, sh, iax, iay, iaz)) {
+                if (skip_cell(R, w, sh)) {
                     if (STATS) st.skips++;
                     continue;
                 }
                 if (STATS) st.skip_out++;
             }
             // step through the cell without lookups (budget ends inside it, or not exact)
-            const uint32_t ewx = wx, ewy = wy, ewz = wz;
+            const uint32_t c[3] = {w[0], w[1], w[2]};
             bool left = false;
             while (R.steps > 0) {
                 dda_step(R);
                 if (STATS) st.plain_steps++;
-                wx = (uint32_t)R.rx & wm;
-                wy = (uint32_t)R.ry & wm;
-                wz = (uint32_t)R.rz & wm;
-                if ((((wx ^ ewx) | (wy ^ ewy) | (wz ^ ewz)) >> sh) != 0u) {
+                wrap3(R, wm, w);
+                if (!same_cell(w, c, sh)) {
                     left = true;
                     break;
                 }
             }
             if (!left) break;
         }
-    }
     }
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
@@ -497,21 +401,21 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Node* __restrict
         atomicAdd(P.stats + 6, (unsigned long long)st.plain_steps);
     }
     Hit h;
-    h.x = R.rx;
-    h.y = R.ry;
-    h.z = R.rz;
+    h.x = R.r[0];
+    h.y = R.r[1];
+    h.z = R.r[2];
     h.steps_left = hit ? R.steps : 0;
     h.t = (float)R.tlast;
-    uint32_t neg = 0u;
-    if (R.axis == 0u) neg = R.sx < 0;
-    else if (R.axis == 1u) neg = R.sy < 0;
-    else if (R.axis == 2u) neg = R.sz < 0;
+    const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
+    const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
     h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (mat & MAT_MASK);
     return h;
 }
 
-template <bool STATS, bool FLAT>
+template <bool STATS>
 __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(P.nodes), (short)0, (int)0x7FFFFFFF, (int)0x00020000);
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
     if (STATS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
@@ -571,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS, FLAT>(P, lds, nlds, o, d);
+        const Hit h = trace<STATS>(P, rsrc, lds, nlds, o, d);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -700,14 +604,10 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
-    const bool flat = (P.flags & SVO_CAST_FLAT) != 0;
-    if (P.flags & SVO_CAST_STATS) {
-        if (flat) hipLaunchKernelGGL((k_cast<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-        else hipLaunchKernelGGL((k_cast<true, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-    } else {
-        if (flat) hipLaunchKernelGGL((k_cast<false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-        else hipLaunchKernelGGL((k_cast<false, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-    }
+    if (P.flags & SVO_CAST_STATS)
+        hipLaunchKernelGGL(k_cast<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    else
+        hipLaunchKernelGGL(k_cast<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -736,7 +636,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL((k_cast<false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL(k_cast<false>, dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
