@@ -156,9 +156,9 @@ typedef struct {
 #define SVO_CAST_ITERATIVE 1
 /* svo_cast_desc.flags: accumulate traversal counters into svo_cast_desc.stats (diagnostics) */
 #define SVO_CAST_STATS 2
-/* svo_cast_desc.flags, scheduling experiment (results identical): dispatch the frame's top tile
-   rows first */
-#define SVO_CAST_TOP_FIRST 4
+/* svo_cast_desc.flags, scheduling (results identical): frames are dispatched top tile row first
+   (longest rays first); this bit restores bottom-first order */
+#define SVO_CAST_BOTTOM_FIRST 4
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
 #define SVO_CAST_XCD_SWIZZLE 16
 

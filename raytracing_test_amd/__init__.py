@@ -21,7 +21,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsvo_rt.so")
+LIB_PATH = os.environ.get("SVO_LIB") or os.path.join(_HERE, "libsvo_rt.so")
 
 SVO_OK = 0
 HIT_BIT = 1 << 31
@@ -33,7 +33,7 @@ MAT_MASK = 0xFFFF
 NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
 CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B reference path)
 CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.stats
-CAST_TOP_FIRST = 4  # scheduling experiment: top tile rows first
+CAST_BOTTOM_FIRST = 4  # scheduling: bottom tile rows first (default is top first)
 CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64")

@@ -31,28 +31,31 @@ def _run(cmd):
     subprocess.check_call(cmd)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=None, build_dir=None, defines=()):
+    """out / build_dir / defines: alternate variants for A/B timing (the default is the product)"""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
-    os.makedirs(BUILD, exist_ok=True)
+    OUT_ = out or OUT
+    BUILD_ = build_dir or BUILD
+    os.makedirs(BUILD_, exist_ok=True)
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "svo_rt.h")]
     objs = []
     for s in HOST_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(BUILD, s + ".o")
+        obj = os.path.join(BUILD_, s + ".o")
         if force or _newer(obj, [src] + hdrs):
             _run(["g++", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-Wall",
                   "-c", src, "-o", obj])
         objs.append(obj)
     for s in HIP_SRCS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(BUILD, s + ".o")
+        obj = os.path.join(BUILD_, s + ".o")
         if force or _newer(obj, [src] + hdrs):
             _run([hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
-                  "-Wall", "-c", src, "-o", obj])
+                  "-Wall"] + ["-D" + d for d in defines] + ["-c", src, "-o", obj])
         objs.append(obj)
-    if force or _newer(OUT, objs):
-        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT] + objs + ["-pthread"])
-    return OUT
+    if force or _newer(OUT_, objs):
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT_] + objs + ["-pthread"])
+    return OUT_
 
 
 if __name__ == "__main__":

@@ -413,7 +413,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
+#ifndef SVO_MIN_WAVES
+#define SVO_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams P) {
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(P.nodes), (short)0, (int)0x7FFFFFFF, (int)0x00020000);
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
@@ -440,7 +443,9 @@ __global__ __launch_bounds__(kBlock) void k_cast(const CastParams P) {
         const int64_t tile = g >> 6;
         const int32_t lane = (int32_t)(g & 63);
         int32_t trl = (int32_t)(tile / P.tiles_x);
-        if (P.flags & SVO_CAST_TOP_FIRST) trl = P.tile_rows_local - 1 - trl;
+        // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
+        // them first keeps the long tiles out of the launch's tail)
+        if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - (int64_t)(tile / P.tiles_x) * P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         const int32_t px = tx * 8 + (lane & 7), py = tr * 8 + (lane >> 3);

@@ -65,7 +65,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     W = H = 256
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_TOP_FIRST):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
