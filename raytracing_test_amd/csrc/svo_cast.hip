@@ -122,12 +122,13 @@ __device__ __forceinline__ int32_t count_before(double T, double a, float inva, 
 struct Ray {
     int32_t r[3];   // current voxel (unwrapped)
     double T[3];    // next crossing per axis (deltaPos)
-    double a[3];    // absDelta
+    float af[3];    // absDelta: an f32 value widened to f64 by the reference (ray_caster.cpp:35-41)
     float ia[3];    // 1/absDelta estimate (counts only)
     int32_t s[3];   // step
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
-    double tlast;   // crossing value of the last step
+    float tlast;    // crossing value of the last step, as output (f32)
+    __device__ __forceinline__ double a(int k) const { return (double)af[k]; }
 };
 
 // one DDA step (ray_caster.cpp:70-80), branch-free
@@ -135,14 +136,14 @@ __device__ __forceinline__ void dda_step(Ray& R) {
     const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
     const bool cy = !cx && (R.T[1] < R.T[2]);
     const bool cz = !cx && !cy;
-    R.tlast = cx ? R.T[0] : (cy ? R.T[1] : R.T[2]);
+    R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
     R.axis = cx ? 0u : (cy ? 1u : 2u);
     R.r[0] += cx ? R.s[0] : 0;
     R.r[1] += cy ? R.s[1] : 0;
     R.r[2] += cz ? R.s[2] : 0;
-    R.T[0] = cx ? R.T[0] + R.a[0] : R.T[0];
-    R.T[1] = cy ? R.T[1] + R.a[1] : R.T[1];
-    R.T[2] = cz ? R.T[2] + R.a[2] : R.T[2];
+    R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+    R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+    R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
     R.steps--;
 }
 
@@ -161,7 +162,7 @@ __device__ __forceinline__ bool skip_cell(Ray& R, const uint32_t w[3], uint32_t 
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         e[k] = min(exit_steps(w[k], R.s[k], sh), lim);
-        E[k] = R.T[k] + (double)(e[k] - 1) * R.a[k];
+        E[k] = R.T[k] + (double)(e[k] - 1) * R.a(k);
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
@@ -173,7 +174,7 @@ __device__ __forceinline__ bool skip_cell(Ray& R, const uint32_t w[3], uint32_t 
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         // axis k's events tied with V come after the exit event when rank_k > rank_b (k < b)
-        const int32_t c = count_before(R.T[k], R.a[k], R.ia[k], V, (uint32_t)k < b);
+        const int32_t c = count_before(R.T[k], R.a(k), R.ia[k], V, (uint32_t)k < b);
         n[k] = (uint32_t)k == b ? e[k] : c;
         total += n[k];
     }
@@ -181,9 +182,9 @@ __device__ __forceinline__ bool skip_cell(Ray& R, const uint32_t w[3], uint32_t 
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.r[k] += R.s[k] * n[k];
-        R.T[k] += (double)n[k] * R.a[k];
+        R.T[k] += (double)n[k] * R.a(k);
     }
-    R.tlast = V;
+    R.tlast = (float)V;
     R.axis = b;
     R.steps -= total;
     return true;
@@ -306,15 +307,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         const Dda1 ax = dda_axis(o[k], d[k]);
         R.r[k] = ax.cell;
         R.T[k] = ax.dpos;
-        R.a[k] = ax.adelta;
+        R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
         R.s[k] = ax.step;
         R.ia[k] = (float)(1.0 / ax.adelta);
     }
     R.steps = P.steps;
     R.axis = 3u;
-    R.tlast = 0.0;
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a[0], P.steps) && exact_axis(R.T[1], R.a[1], P.steps) &&
-                      exact_axis(R.T[2], R.a[2], P.steps);
+    R.tlast = 0.0f;
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a(0), P.steps) && exact_axis(R.T[1], R.a(1), P.steps) &&
+                      exact_axis(R.T[2], R.a(2), P.steps);
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -405,7 +406,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     h.y = R.r[1];
     h.z = R.r[2];
     h.steps_left = hit ? R.steps : 0;
-    h.t = (float)R.tlast;
+    h.t = R.tlast;
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
     h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (mat & MAT_MASK);
@@ -414,7 +415,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 
 template <bool STATS>
 #ifndef SVO_MIN_WAVES
-#define SVO_MIN_WAVES 1
+#define SVO_MIN_WAVES 6  // 80 VGPRs: 6 waves per SIMD without spills
 #endif
 __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams P) {
     const __amdgpu_buffer_rsrc_t rsrc =
