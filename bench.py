@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
+    ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     args = ap.parse_args()
 
@@ -142,9 +143,11 @@ def main():
     n_pad = shard.max_shard_count(W, H, world)
     for f in range(nframes):
         d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
-                               flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags)
+                               flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao)
         descs.append(d)
         flat, views = shard.alloc_flat(n_pad, torch.device("cuda", dev))
+        if args.ao:
+            views["ao"] = torch.zeros(n_pad, dtype=torch.uint8, device=torch.device("cuda", dev))
         flats.append(flat)
         outs.append(views)
     stream = torch.cuda.Stream(device=dev)
@@ -229,7 +232,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_ray": round(b_ray, 2), "avg_launch_ms": round(avg_kernel_s * 1e3, 4)}
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and not args.ao:
         hits = rt.decode_hits(outs[0])
         cpu = cpu_baseline(ppx, ppy, hits)
     line = {
@@ -245,7 +248,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols),
-        "config": {"workload": "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080 primary rays per GPU per "
+        "config": {"ao_samples": args.ao, "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") + "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080 primary rays per GPU per "
                                "step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % (args.cols, STEPS),
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
                    "gather": world > 1 and not args.no_gather, "tree_nodes": info.n_nodes,

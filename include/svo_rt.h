@@ -125,11 +125,17 @@ void svo_tree_destroy(svo_tree* t);
      info[i]                 = bit 31 hit | bits 16-17 last axis (3 = no step) | bit 18 step < 0
                                on that axis | bits 0-15 material id (0 = none)
    RayResult.lastPos = pos - (axis step).  Frame rays: index = row * width + px, rows counted
-   from the bottom (gl_FragCoord), restricted to the tile rows of this shard. */
+   from the bottom (gl_FragCoord), restricted to the tile rows of this shard.
+   Hemisphere AO (light_scattering.frag:133-236): for a hit, ao_samples rays
+   start at the centre of lastPos, directions = svo_hemisphere's table with its pole (component 2)
+   turned to the hit face's normal by a signed axis permutation (pole -> normal axis, components
+   0/1 -> the next two axes cyclically), each cast with castRayFromCam semantics and ao_steps
+   steps; ao[i] = number of them that hit. */
 typedef struct {
     int32_t* pos_steps;
     float* t;
     uint32_t* info;
+    uint8_t* ao;       /* per ray: AO rays that hit (0..ao_samples); required when ao_samples > 0 */
 } svo_hits;
 
 typedef struct {
@@ -145,6 +151,8 @@ typedef struct {
     int32_t n_rays;
     int32_t steps;     /* DDA step budget per ray (castRayFromCam's `steps`) */
     int32_t flags;     /* SVO_CAST_* bits, 0 = default */
+    int32_t ao_samples; /* hemisphere AO rays per primary hit (0 = off, <= 64; reference: 20) */
+    int32_t ao_steps;   /* DDA budget of each AO ray (reference: 5, light_scattering.frag:231) */
     uint64_t* stats;   /* optional device u64[16] accumulating per-launch counters when
                           flags & SVO_CAST_STATS: rays, lookups, node loads, cell skips,
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
@@ -178,6 +186,9 @@ int svo_pixel_dir(const float cam_dir[3], float ppx, float ppy, int32_t width, i
                   float out[3]);
 /* every pixel's direction, out[3 * (py * width + px) + a] */
 int svo_pixel_dirs(const float cam_dir[3], float ppx, float ppy, int32_t width, int32_t height, float* out);
+/* gen_hemisphare_distrib.py's table for n points (x, y, pole) as float: phi = acos(1-(i+.5)*.85/n),
+   theta = pi*(1+sqrt 5)*(i+.5) */
+int svo_hemisphere(int32_t n, float* out);
 
 #ifdef __cplusplus
 }

@@ -1103,3 +1103,100 @@ EXPORT int orc_dump_box(const otree* t, int x0, int y0, int z0, int nx, int ny, 
             }
     return err ? -1 : 0;
 }
+
+/* ------------------------------------------------------------------------------------------------
+ * Hemisphere AO (light_scattering.frag:133-154,175-236; gen_hemisphare_distrib.py)
+ * Table: phi = arccos(1 - (i+0.5)*0.85/N), theta = pi*(1+sqrt 5)*(i+0.5); (cos th sin ph,
+ * sin th sin ph, cos ph) in double, rounded to float; component 2 is the pole (the shader reads the
+ * printed (x, z, y) back through .xzy, so its pole is +z).  The reference computes an orientation
+ * matrix but never applies it (light_scattering.frag:224 vs :231); this build orients the pole to
+ * the hit face's normal by an exact signed axis permutation.  Each AO ray starts at the centre of
+ * lastPos and is a castRayFromCam with a 5-step budget (light_scattering.frag:231); the pixel's
+ * result is the number of AO rays that hit.
+ * ---------------------------------------------------------------------------------------------- */
+EXPORT void orc_hemisphere(int n, float* out) {
+    const double PI = 3.141592653589793;
+    for (int i = 0; i < n; i++) {
+        double idx = (double)i + 0.5;
+        double phi = acos(1.0 - idx * 0.85 / (double)n);
+        double theta = PI * (1.0 + sqrt(5.0)) * idx;
+        out[3 * i + 0] = (float)(cos(theta) * sin(phi));
+        out[3 * i + 1] = (float)(sin(theta) * sin(phi));
+        out[3 * i + 2] = (float)cos(phi);
+    }
+}
+
+/* AO direction for a face normal on axis `ax` with sign `sg` (+1/-1): pole -> ax, then the two
+   tangent components to the cyclically following axes */
+static inline void o_ao_dir(const float h[3], int ax, int sg, float d[3]) {
+    d[ax] = sg > 0 ? h[2] : -h[2];
+    d[(ax + 1) % 3] = h[0];
+    d[(ax + 2) % 3] = h[1];
+}
+
+static int o_ao_count(o_getblock_fn gb, const void* world, const orayres* P, const float* table, int n, int steps) {
+    if (!P->hit || P->axis < 0) return 0;
+    int ax = P->axis;
+    int sg = P->last[ax] - P->pos[ax]; /* normal points from the hit voxel towards lastPos */
+    float org[3] = {(float)P->last[0] + 0.5f, (float)P->last[1] + 0.5f, (float)P->last[2] + 0.5f};
+    int cnt = 0;
+    for (int i = 0; i < n; i++) {
+        float d[3];
+        o_ao_dir(table + 3 * i, ax, sg, d);
+        orayres R;
+        o_cast(gb, world, org, d, steps, &R);
+        cnt += R.hit != 0;
+    }
+    return cnt;
+}
+
+typedef struct {
+    const otree* t;
+    float org[3], cam[3], ppx, ppy, rw, rh;
+    int W, H, steps, tid, nthreads, n_ao, ao_steps;
+    const float* table;
+    const int64_t* pix;
+    int64_t n;
+    uint8_t* ao;
+    int32_t* hit;
+} o_aojob;
+static void* o_ao_worker(void* p) {
+    o_aojob* j = (o_aojob*)p;
+    for (int64_t k = j->tid; k < j->n; k += j->nthreads) {
+        int64_t pi = j->pix ? j->pix[k] : k;
+        float d[3];
+        o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
+        orayres R;
+        o_cast(o_gb_tree, j->t, j->org, d, j->steps, &R);
+        j->ao[k] = (uint8_t)o_ao_count(o_gb_tree, j->t, &R, j->table, j->n_ao, j->ao_steps);
+        if (j->hit) j->hit[k] = R.hit;
+    }
+    return NULL;
+}
+EXPORT void orc_cast_frame_ao(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
+                              int n_ao, int ao_steps, const int64_t* pix, int64_t n, int nthreads, uint8_t* ao, int32_t* hit) {
+    float table[3 * 64];
+    if (n_ao > 64) n_ao = 64;
+    orc_hemisphere(n_ao, table);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    o_aojob* jobs = (o_aojob*)calloc((size_t)nthreads, sizeof(o_aojob));
+    for (int i = 0; i < nthreads; i++) {
+        o_aojob* j = &jobs[i];
+        j->t = t;
+        memcpy(j->org, org, 12);
+        memcpy(j->cam, cam, 12);
+        j->ppx = ppx; j->ppy = ppy;
+        j->rw = 1.0f / (float)W; j->rh = 1.0f / (float)H;
+        j->W = W; j->H = H; j->steps = steps; j->n_ao = n_ao; j->ao_steps = ao_steps;
+        j->table = table;
+        j->pix = pix;
+        j->n = pix ? n : (int64_t)W * H;
+        j->tid = i; j->nthreads = nthreads;
+        j->ao = ao; j->hit = hit;
+        pthread_create(&th[i], NULL, o_ao_worker, j);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(jobs);
+}

@@ -119,6 +119,9 @@ def lib(native=False):
     L.orc_digest_box.restype = C.c_uint64
     L.orc_digest_box.argtypes = [vp] + [C.c_int] * 6
     L.orc_dump_box.argtypes = [vp] + [C.c_int] * 6 + [_u32p, _u64p]
+    L.orc_hemisphere.argtypes = [C.c_int, _f32p]
+    L.orc_cast_frame_ao.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                    C.c_int, vp, vp]
     _libs[path] = L
     return L
 
@@ -147,6 +150,12 @@ def pixel_dir(cam, ppx, ppy, W, H, px, py):
     o = np.zeros(3, np.float32)
     lib().orc_pixel_dir(f3(cam), ppx, ppy, W, H, px, py, o)
     return o
+
+
+def hemisphere(n):
+    out = np.zeros(3 * n, np.float32)
+    lib().orc_hemisphere(n, out)
+    return out.reshape(n, 3)
 
 
 def noise2(seed, x, y):
@@ -255,6 +264,18 @@ class Tree:
         out["rc"] = rc
         out["dda_steps"] = dda.value
         return out
+
+    def cast_frame_ao(self, org, cam, W, H, steps, n_ao, ao_steps=5, ppx=None, ppy=None, pixels=None, nthreads=8):
+        """primary rays + hemisphere AO: per-pixel count of AO rays that hit (see oracle.c A8)"""
+        if ppx is None:
+            ppx, ppy = proj_plane(W, H)
+        n = W * H if pixels is None else len(pixels)
+        pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
+        ao = np.zeros(n, np.uint8)
+        hit = np.zeros(n, np.int32)
+        self.L.orc_cast_frame_ao(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, n_ao, ao_steps, _ptr(pix), n, nthreads, _ptr(ao),
+                                 _ptr(hit))
+        return ao, hit
 
     def frame_entries(self, org, cam, W, H, steps, ppx=None, ppy=None, pixels=None, nthreads=8):
         if ppx is None:

@@ -89,12 +89,14 @@ class CastDesc(C.Structure):
         ("n_rays", C.c_int32),
         ("steps", C.c_int32),
         ("flags", C.c_int32),
+        ("ao_samples", C.c_int32),
+        ("ao_steps", C.c_int32),
         ("stats", C.c_void_p),
     ]
 
 
 class Hits(C.Structure):
-    _fields_ = [("pos_steps", C.c_void_p), ("t", C.c_void_p), ("info", C.c_void_p)]
+    _fields_ = [("pos_steps", C.c_void_p), ("t", C.c_void_p), ("info", C.c_void_p), ("ao", C.c_void_p)]
 
 
 _lib = None
@@ -106,7 +108,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain", "svo_tree_get_info", "svo_tree_palette", "svo_tree_get_block", "svo_tree_export",
     "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
-    "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights",
+    "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere",
 )
 
 
@@ -159,6 +161,7 @@ def lib():
     L.svo_tree_get_blocks.argtypes = [vp, vp, C.c_int64, vp]
     L.svo_noise2.argtypes = [C.c_int64, vp, vp, C.c_int64, vp]
     L.svo_terrain_heights.argtypes = [i32, i32, i32, vp]
+    L.svo_hemisphere.argtypes = [i32, vp]
     _lib = L
     return L
 
@@ -200,6 +203,13 @@ def pixel_dirs(cam_dir, width, height, ppx=None, ppy=None):
         ppx, ppy = proj_plane(width, height)
     out = np.zeros((height, width, 3), np.float32)
     _check(lib().svo_pixel_dirs(_f3(cam_dir), ppx, ppy, width, height, out.ctypes.data_as(C.c_void_p)), "svo_pixel_dirs")
+    return out
+
+
+def hemisphere(n):
+    """gen_hemisphare_distrib.py's sample table for n points, (n, 3) float32 as (x, y, pole)"""
+    out = np.zeros((n, 3), np.float32)
+    _check(lib().svo_hemisphere(n, out.ctypes.data_as(C.c_void_p)), "svo_hemisphere")
     return out
 
 
@@ -363,7 +373,8 @@ class Tree:
 
     # ------------------------------------------------------------------------------ casting --
     @staticmethod
-    def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1, flags=0):
+    def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1, flags=0,
+                   ao_samples=0, ao_steps=5):
         if ppx is None:
             ppx, ppy = proj_plane(width, height)
         d = CastDesc()
@@ -373,6 +384,8 @@ class Tree:
         d.tile_row_start, d.tile_row_step = tile_row_start, tile_row_step
         d.steps = steps
         d.flags = flags
+        d.ao_samples = ao_samples
+        d.ao_steps = ao_steps
         return d
 
     @staticmethod
@@ -382,27 +395,32 @@ class Tree:
         return n.value
 
     @staticmethod
-    def alloc_hits(n, device):
+    def alloc_hits(n, device, ao=False):
         torch = _torch()
         dev = torch.device("cuda", device)
-        return dict(
+        out = dict(
             pos_steps=torch.empty((n, 4), dtype=torch.int32, device=dev),
             t=torch.empty(n, dtype=torch.float32, device=dev),
             info=torch.empty(n, dtype=torch.int32, device=dev),
         )
+        if ao:
+            out["ao"] = torch.empty(n, dtype=torch.uint8, device=dev)
+        return out
 
     def cast(self, desc, out, stream=None):
         """Launch the cast kernel asynchronously on `stream` (a torch.cuda.Stream or raw handle)."""
-        h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr())
+        ao = out.get("ao")
+        h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), ao.data_ptr() if ao is not None else None)
         s = getattr(stream, "cuda_stream", stream)
         _check(lib().svo_cast_rays(self._h, C.byref(desc), C.byref(h), C.c_void_p(s) if s else None), "svo_cast_rays")
 
     def cast_frame(self, origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1,
-                   out=None, stream=None, sync=True, flags=0):
-        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step, flags)
+                   out=None, stream=None, sync=True, flags=0, ao_samples=0, ao_steps=5):
+        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step, flags, ao_samples,
+                            ao_steps)
         n = self.count(d)
         if out is None:
-            out = self.alloc_hits(n, self.info().device)
+            out = self.alloc_hits(n, self.info().device, ao=ao_samples > 0)
         self.cast(d, out, stream)
         if sync:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
@@ -444,5 +462,8 @@ def decode_hits(out):
     for a in range(3):
         sel = axis == a
         last[sel, a] -= np.where(neg[sel], -1, 1)
-    return dict(pos=pos, last_pos=last, steps=ps[:, 3].copy(), hit=(info & HIT_BIT) != 0, axis=axis.astype(np.int32),
-                material=(info & MAT_MASK).astype(np.int32), t=t)
+    res = dict(pos=pos, last_pos=last, steps=ps[:, 3].copy(), hit=(info & HIT_BIT) != 0, axis=axis.astype(np.int32),
+               material=(info & MAT_MASK).astype(np.int32), t=t)
+    if out.get("ao") is not None:
+        res["ao"] = out["ao"].cpu().numpy()
+    return res

@@ -62,6 +62,10 @@ struct CastParams {
     int32_t* pos;
     float* t;
     uint32_t* info;
+    uint8_t* ao;
+    // hemisphere AO (A8)
+    int32_t ao_n, ao_steps;
+    float ao_tab[3 * 64];
 };
 
 constexpr int kBlock = 256;
@@ -300,7 +304,7 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 // One ray with castRayFromCam semantics.
 template <bool STATS>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                     uint32_t nlds, const float o[3], const float d[3]) {
+                                     uint32_t nlds, const float o[3], const float d[3], int32_t budget) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -311,11 +315,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         R.s[k] = ax.step;
         R.ia[k] = (float)(1.0 / ax.adelta);
     }
-    R.steps = P.steps;
+    R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a(0), P.steps) && exact_axis(R.T[1], R.a(1), P.steps) &&
-                      exact_axis(R.T[2], R.a(2), P.steps);
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
+                      exact_axis(R.T[2], R.a(2), budget);
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -427,6 +431,9 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     __shared__ Node lds[kLdsNodes];
     const uint32_t nlds = P.lds_nodes;
     for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
+    // hemisphere AO sample set, broadcast from LDS
+    __shared__ float ao_tab[3 * 64];
+    for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
     int64_t blk = blockIdx.x;
     if (P.flags & SVO_CAST_XCD_SWIZZLE) {
@@ -481,10 +488,28 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, lds, nlds, o, d);
+        const Hit h = trace<STATS>(P, rsrc, lds, nlds, o, d, P.steps);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
+        if (P.ao_n > 0) {
+            // AO rays from the centre of lastPos, pole turned to the hit face's normal (A8)
+            uint32_t cnt = 0u;
+            if (h.info & HIT_BIT) {
+                const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
+                const int32_t st = (h.info & NEG_BIT) ? -1 : 1;  // step on the hit axis
+                const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
+                const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
+                for (int32_t i = 0; i < P.ao_n; i++) {
+                    const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
+                    float ad[3];
+                    ao_dir(hv, ax, -st, ad);
+                    const Hit a = trace<false>(P, rsrc, lds, nlds, ao_o, ad, P.ao_steps);
+                    cnt += (a.info & HIT_BIT) ? 1u : 0u;
+                }
+            }
+            P.ao[out] = (uint8_t)cnt;
+        }
     }
     if (STATS) {
         __syncthreads();
@@ -512,6 +537,10 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.pos = o->pos_steps;
     P.t = o->t;
     P.info = o->info;
+    P.ao = o->ao;
+    P.ao_n = d->ao_samples;
+    P.ao_steps = d->ao_steps;
+    if (P.ao_n > 0) hemisphere_table(P.ao_n, P.ao_tab);
     if (d->ray_dirs) {
         P.mode = MODE_EXPLICIT;
         P.rdir = d->ray_dirs;
@@ -597,6 +626,8 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_rays: tree not uploaded (svo_upload)");
     if (d->steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative step budget");
     if ((d->flags & SVO_CAST_STATS) && !d->stats) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: SVO_CAST_STATS without a stats buffer");
+    if (d->ao_samples < 0 || d->ao_samples > 64) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: ao_samples must be in [0, 64]");
+    if (d->ao_samples > 0 && (!o->ao || d->ao_steps < 0)) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: AO needs an ao buffer and ao_steps >= 0");
     if (d->ray_dirs) {
         if (d->n_rays < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative ray count");
     } else if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0) {

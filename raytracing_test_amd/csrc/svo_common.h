@@ -9,8 +9,10 @@
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define SVO_HD __host__ __device__ __forceinline__
+#define SVO_HOST __host__ static inline
 #else
 #define SVO_HD static inline
+#define SVO_HOST static inline
 #endif
 
 namespace svo {
@@ -133,6 +135,29 @@ SVO_HD Dda1 dda_axis(float o, float d) {
     if (r.step < 0) exact -= 1.0;
     r.dpos = r.adelta - (exact - (double)r.cell) * delta;
     return r;
+}
+
+// gen_hemisphare_distrib.py:4-13 — Fibonacci-spiral hemisphere, polar span 0.85, evaluated in
+// double and rounded to float; (x, y, pole).  Host only (libm).
+SVO_HOST void hemisphere_table(int32_t n, float* out) {
+    const double pi = 3.141592653589793;
+    for (int32_t i = 0; i < n; i++) {
+        const double idx = (double)i + 0.5;
+        const double phi = __builtin_acos(1.0 - idx * 0.85 / (double)n);
+        const double theta = pi * (1.0 + __builtin_sqrt(5.0)) * idx;
+        out[3 * i + 0] = (float)(__builtin_cos(theta) * __builtin_sin(phi));
+        out[3 * i + 1] = (float)(__builtin_sin(theta) * __builtin_sin(phi));
+        out[3 * i + 2] = (float)__builtin_cos(phi);
+    }
+}
+
+// AO direction: the table entry's pole turned to axis `ax` (sign sg), its first two components to
+// the next two axes cyclically.  Exact (a permutation and a sign).
+SVO_HD void ao_dir(const float h[3], uint32_t ax, int32_t sg, float d[3]) {
+    const float p = sg > 0 ? h[2] : -h[2];
+    d[0] = ax == 0u ? p : (ax == 1u ? h[1] : h[0]);
+    d[1] = ax == 1u ? p : (ax == 2u ? h[1] : h[0]);
+    d[2] = ax == 2u ? p : (ax == 0u ? h[1] : h[0]);
 }
 
 }  // namespace svo

@@ -806,6 +806,12 @@ extern "C" int svo_pixel_dirs(const float cam[3], float ppx, float ppy, int32_t 
     return SVO_OK;
 }
 
+extern "C" int svo_hemisphere(int32_t n, float* out) {
+    if (n < 0 || n > 64 || (!out && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_hemisphere: n must be in [0, 64]");
+    hemisphere_table(n, out);
+    return SVO_OK;
+}
+
 extern "C" int svo_noise2(int64_t seed, const double* x, const double* y, int64_t n, double* out) {
     if ((!x || !y || !out) && n > 0) SVO_FAIL(SVO_EINVAL, "svo_noise2: NULL argument");
     Simplex2 s;

@@ -269,3 +269,25 @@ def test_depth12_full_frame_properties(rt, depth12):
     used = 16384 - a["steps"]
     l1 = np.abs(a["pos"] - np.array([4, 90, 4])).sum(1)
     assert np.array_equal(l1[a["hit"]], used[a["hit"]])
+
+
+@pytest.mark.parametrize("n_ao", [16, 20])
+def test_ao_reference_world(rt, gtree, ref_world_oracle, n_ao):
+    """A8 / C4: hemisphere AO counts (per pixel, rays that hit within 5 steps) against the oracle."""
+    for org, d in CAMERAS[:3]:
+        dn = rt.normalize(d)
+        out = rt.decode_hits(gtree.cast_frame(org, dn, 128, 128, 300, ao_samples=n_ao, ao_steps=5))
+        ao, hit = ref_world_oracle.cast_frame_ao(org, dn, 128, 128, 300, n_ao, 5)
+        assert np.array_equal(out["hit"], hit != 0)
+        assert np.array_equal(out["ao"], ao), (org, n_ao)
+        assert out["ao"].max() <= n_ao
+
+
+def test_ao_depth12_sampled(rt, oracle_mod, depth12):
+    T = oracle_mod.Tree.terrain(6, 4096, 4096)
+    dn = rt.normalize([1, -0.45, 1])
+    out = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=16, ao_steps=5))
+    pix = np.random.default_rng(2).integers(0, 1920 * 1080, 3000)
+    ao, hit = T.cast_frame_ao((4, 90, 4), dn, 1920, 1080, 16384, 16, 5, pixels=pix, nthreads=16)
+    assert np.array_equal(out["ao"][pix], ao)
+    assert out["ao"].mean() > 0.5  # terrain occludes part of the hemisphere
