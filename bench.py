@@ -197,27 +197,31 @@ def main():
 
     if args.stats and rank == 0:
         nblk = (rt.Tree.count(descs[0]) + 255) // 256
-        st = torch.zeros(16 + 2 * nblk, dtype=torch.int64, device=dev)
         d0 = descs[0]
-        d0.flags |= rt.CAST_STATS
-        d0.stats = st.data_ptr()
-        tree.cast(d0, outs[0], stream)
-        torch.cuda.synchronize()
-        d0.flags &= ~rt.CAST_STATS
-        allv = st.cpu().numpy()
-        vals = allv[:16]
-        stamps = allv[16:].reshape(-1, 2).astype(np.float64) / 100.0  # us (s_memrealtime = 100 MHz)
-        t0s = stamps[:, 0].min()
-        dur = stamps[:, 1] - stamps[:, 0]
-        span = stamps[:, 1].max() - t0s
-        # blocks resident over time (16 bins) and the mean duration per tenth of the block order
-        bins = np.linspace(0, span, 17)
-        res = [int(((stamps[:, 0] - t0s < b1) & (stamps[:, 1] - t0s > b0)).sum()) for b0, b1 in zip(bins[:-1], bins[1:])]
-        tenths = [float(np.mean(c)) for c in np.array_split(dur, 10)]
-        print("timeline: span %.1f us, mean block %.1f us, max %.1f us, resident blocks per 1/16 span %s, mean block us per tenth of grid %s"
-              % (span, dur.mean(), dur.max(), res, ["%.0f" % x for x in tenths]), file=sys.stderr)
-        print("stats per ray: " + ", ".join("%s=%.3f" % (k, v / max(1, vals[0])) for k, v in zip(rt.STAT_NAMES, vals)) +
-              "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
+        for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
+            st = torch.zeros(16 + 2 * nblk, dtype=torch.int64, device=dev)
+            d0.flags |= mode
+            d0.stats = st.data_ptr()
+            tree.cast(d0, outs[0], stream)
+            torch.cuda.synchronize()
+            d0.flags &= ~mode
+            allv = st.cpu().numpy()
+            if mode == rt.CAST_STATS:
+                vals = allv[:16]
+                print("stats per ray: " + ", ".join("%s=%.3f" % (k, v / max(1, vals[0])) for k, v in zip(rt.STAT_NAMES, vals)) +
+                      "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
+                continue
+            stamps = allv[16:].reshape(-1, 2).astype(np.float64) / 100.0  # us (s_memrealtime = 100 MHz)
+            t0s = stamps[:, 0].min()
+            dur = stamps[:, 1] - stamps[:, 0]
+            span = stamps[:, 1].max() - t0s
+            bins = np.linspace(0, span, 17)
+            res = [int(((stamps[:, 0] - t0s < b1) & (stamps[:, 1] - t0s > b0)).sum()) for b0, b1 in zip(bins[:-1], bins[1:])]
+            tenths = [float(np.mean(c)) for c in np.array_split(dur, 10)]
+            ends = np.sort(stamps[:, 1] - t0s)
+            print("timeline: span %.1f us, mean block %.1f us, max %.1f us, last 10%% of blocks end after %.1f us; blocks overlapping "
+                  "each 1/16 of the span %s; mean block us per tenth of the grid %s"
+                  % (span, dur.mean(), dur.max(), ends[int(len(ends) * 0.9)], res, ["%.0f" % x for x in tenths]), file=sys.stderr)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

@@ -156,7 +156,8 @@ typedef struct {
     uint64_t* stats;   /* optional device u64[16] accumulating per-launch counters when
                           flags & SVO_CAST_STATS: rays, lookups, node loads, cell skips,
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
-                          lane work units, wave-max work units x 64 */
+                          lane work units, wave-max work units x 64; then 2 stamps per block
+                          (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
 
 /* svo_cast_desc.flags: take every DDA step one at a time (disables the exact closed-form crossing
@@ -167,6 +168,8 @@ typedef struct {
 /* svo_cast_desc.flags, scheduling (results identical): frames are dispatched top tile row first
    (longest rays first); this bit restores bottom-first order */
 #define SVO_CAST_BOTTOM_FIRST 4
+/* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[16 + 2*block] only */
+#define SVO_CAST_TIMELINE 32
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
 #define SVO_CAST_XCD_SWIZZLE 16
 

@@ -35,6 +35,7 @@ CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B referenc
 CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.stats
 CAST_BOTTOM_FIRST = 4  # scheduling: bottom tile rows first (default is top first)
 CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
+CAST_TIMELINE = 32  # per-block start/end stamps only
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64")
 

@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         __builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(P.nodes), (short)0, (int)0x7FFFFFFF, (int)0x00020000);
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
-    if (STATS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
+    if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     // top of the breadth-first array (root + the first levels) staged in LDS
     __shared__ Node lds[kLdsNodes];
     const uint32_t nlds = P.lds_nodes;
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
             P.ao[out] = (uint8_t)cnt;
         }
     }
-    if (STATS) {
+    if (STAMPS) {
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
@@ -625,7 +625,8 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (!o->pos_steps || !o->t || !o->info) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL output buffer");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_rays: tree not uploaded (svo_upload)");
     if (d->steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative step budget");
-    if ((d->flags & SVO_CAST_STATS) && !d->stats) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: SVO_CAST_STATS without a stats buffer");
+    if ((d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) && !d->stats)
+        SVO_FAIL(SVO_EINVAL, "svo_cast_rays: SVO_CAST_STATS / TIMELINE without a stats buffer");
     if (d->ao_samples < 0 || d->ao_samples > 64) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: ao_samples must be in [0, 64]");
     if (d->ao_samples > 0 && (!o->ao || d->ao_steps < 0)) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: AO needs an ao buffer and ao_steps >= 0");
     if (d->ray_dirs) {
@@ -642,9 +643,11 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
     if (P.flags & SVO_CAST_STATS)
-        hipLaunchKernelGGL(k_cast<true>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+        hipLaunchKernelGGL((k_cast<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    else if (P.flags & SVO_CAST_TIMELINE)
+        hipLaunchKernelGGL((k_cast<false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
     else
-        hipLaunchKernelGGL(k_cast<false>, dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+        hipLaunchKernelGGL((k_cast<false, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -673,7 +676,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL(k_cast<false>, dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL((k_cast<false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
