@@ -417,7 +417,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     return h;
 }
 
-template <bool STATS>
+template <bool STATS, bool STAMPS>
 #ifndef SVO_MIN_WAVES
 #define SVO_MIN_WAVES 6  // 80 VGPRs: 6 waves per SIMD without spills
 #endif
