@@ -328,52 +328,44 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     par.valid = false;
     par.mask = 0ull;
     par.ref = par.sh = par.w[0] = par.w[1] = par.w[2] = 0u;
-    if (R.steps > 0) {
-        dda_step(R);
-        for (;;) {
-            // the voxel just entered is untested
-            uint32_t w[3];
-            wrap3(R, wm, w);
-            uint32_t sh = 0u, bref = 0u, binfo = 0u;
-            uint64_t bmask = 0ull;
-            const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, w, par, sh, bmask, bref, binfo, st);
-            if (kind == R_SOLID) {
-                hit = true;
-                mat = binfo >> 16;
-                break;
-            }
-            if (kind == R_BRICK) {
-                // voxel steps inside the brick, solid mask in registers
-                const uint32_t c[3] = {w[0], w[1], w[2]};
-                bool left = false;
-                for (;;) {
-                    const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
-                    if ((bmask >> v) & 1ull) {
-                        hit = true;
-                        mat = brick_material(P, bmask, bref, binfo, v);
-                        break;
-                    }
-                    if (R.steps <= 0) break;
-                    dda_step(R);
-                    if (STATS) st.brick_steps++;
-                    wrap3(R, wm, w);
-                    if (!same_cell(w, c, 2u)) {
-                        left = true;
-                        break;
-                    }
+    bool done = R.steps <= 0;
+    if (!done) dda_step(R);
+    // one back-edge: every path through the body ends at the loop latch
+    while (!done) {
+        // the voxel just entered is untested
+        uint32_t w[3];
+        wrap3(R, wm, w);
+        uint32_t sh = 0u, bref = 0u, binfo = 0u;
+        uint64_t bmask = 0ull;
+        const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, w, par, sh, bmask, bref, binfo, st);
+        if (kind == R_SOLID) {
+            hit = true;
+            mat = binfo >> 16;
+            done = true;
+        } else if (kind == R_BRICK) {
+            // voxel steps inside the brick, solid mask in registers
+            const uint32_t c[3] = {w[0], w[1], w[2]};
+            for (;;) {
+                const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
+                if ((bmask >> v) & 1ull) {
+                    hit = true;
+                    mat = brick_material(P, bmask, bref, binfo, v);
+                    done = true;
+                    break;
                 }
-                if (hit || !left) break;
-                continue;
-            }
-            // empty cell of size 2^sh around the voxel
-            if (R.steps <= 0) break;
-            if (fast) {
-                if (skip_cell(R, w, sh)) {
-                    if (STATS) st.skips++;
-                    continue;
+                if (R.steps <= 0) {
+                    done = true;
+                    break;
                 }
-                if (STATS) st.skip_out++;
+                dda_step(R);
+                if (STATS) st.brick_steps++;
+                wrap3(R, wm, w);
+                if (!same_cell(w, c, 2u)) break;
             }
+        } else if (R.steps <= 0) {
+            done = true;
+        } else if (!(fast && skip_cell(R, w, sh))) {
+            if (STATS && fast) st.skip_out++;
             // step through the cell without lookups (budget ends inside it, or not exact)
             const uint32_t c[3] = {w[0], w[1], w[2]};
             bool left = false;
@@ -386,7 +378,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                     break;
                 }
             }
-            if (!left) break;
+            done = !left;
+        } else if (STATS) {
+            st.skips++;
         }
     }
     if (STATS) {

@@ -1,0 +1,37 @@
+"""Build libsvo_rt.so from another git revision (or the working tree with -D defines) into variants/
+for A/B timing:  python tools/build_variant.py <name> [--rev REV] [-D NAME=VAL ...]"""
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name")
+    ap.add_argument("--rev", default=None)
+    ap.add_argument("-D", action="append", default=[])
+    a = ap.parse_args()
+    src_root = ROOT
+    tmp = None
+    if a.rev:
+        tmp = tempfile.mkdtemp()
+        subprocess.check_call("git -C %s archive %s raytracing_test_amd include | tar -x -C %s" % (ROOT, a.rev, tmp), shell=True)
+        src_root = tmp
+    sys.path.insert(0, os.path.join(src_root, "raytracing_test_amd"))
+    import build  # noqa
+
+    out = os.path.join(ROOT, "variants", "libsvo_%s.so" % a.name)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    build.build(force=True, out=out, build_dir=os.path.join(ROOT, "variants", "b_" + a.name), defines=a.D)
+    if tmp:
+        shutil.rmtree(tmp)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()
