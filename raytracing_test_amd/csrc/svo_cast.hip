@@ -157,15 +157,57 @@ __device__ __forceinline__ int32_t exit_steps(uint32_t w, int32_t s, uint32_t sh
     return s > 0 ? (int32_t)(lo + (1u << sh) - w) : (int32_t)(w - lo + 1u);
 }
 
-// Cross the empty aligned cell of size 2^sh containing the current voxel in one move, branch-free
-// over the exit axis.  Returns false (state unchanged) when the budget ends inside the cell.
-__device__ __forceinline__ bool skip_cell(Ray& R, const uint32_t w[3], uint32_t sh) {
+// Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
+// the run along x from the mask row, then whole rows along z, then whole planes along y), all from
+// the parent's 64-bit child mask in registers.  Returns per-axis steps to leave the box.
+__device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, int32_t e[3]) {
+    const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
+    // x run through the row (cy, cz)
+    const uint32_t row = (uint32_t)(pmask >> (16u * cz + 4u * cy)) & 0xFu;
+    uint32_t x0, x1;
+    if (s[0] > 0) {
+        const uint32_t n = (uint32_t)__builtin_ctz((row >> cx) | (1u << (4u - cx)));
+        x0 = cx;
+        x1 = cx + n - 1u;
+    } else {
+        const uint32_t below = row & ((1u << cx) - 1u);  // occupied slots below cx
+        x0 = below ? (32u - (uint32_t)__builtin_clz(below)) : 0u;
+        x1 = cx;
+    }
+    const uint32_t xm = ((1u << (x1 + 1u)) - 1u) & ~((1u << x0) - 1u);
+    // whole rows along z
+    uint32_t z0 = cz, z1 = cz;
+    if (s[2] > 0) {
+        while (z1 < 3u && !((uint32_t)(pmask >> (16u * (z1 + 1u) + 4u * cy)) & xm)) z1++;
+    } else {
+        while (z0 > 0u && !((uint32_t)(pmask >> (16u * (z0 - 1u) + 4u * cy)) & xm)) z0--;
+    }
+    // whole planes (x range x z range) along y
+    uint64_t plane = 0ull;
+    for (uint32_t z = z0; z <= z1; z++) plane |= (uint64_t)xm << (16u * z);
+    uint32_t y0 = cy, y1 = cy;
+    if (s[1] > 0) {
+        while (y1 < 3u && !(pmask & (plane << (4u * (y1 + 1u))))) y1++;
+    } else {
+        while (y0 > 0u && !(pmask & (plane << (4u * (y0 - 1u))))) y0--;
+    }
+    const uint32_t lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t base = (w[k] >> (sh + 2u)) << (sh + 2u);
+        e[k] = s[k] > 0 ? (int32_t)(base + ((hi[k] + 1u) << sh) - w[k]) : (int32_t)(w[k] - (base + (lo[k] << sh)) + 1u);
+    }
+}
+
+// Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
+// leave the box.  Returns false (state unchanged) when the budget ends inside the box.
+__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     const int32_t lim = R.steps + 1;  // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
     double E[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        e[k] = min(exit_steps(w[k], R.s[k], sh), lim);
+        e[k] = min(ex[k], lim);
         E[k] = R.T[k] + (double)(e[k] - 1) * R.a(k);
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
@@ -364,7 +406,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             }
         } else if (R.steps <= 0) {
             done = true;
-        } else if (!(fast && skip_cell(R, w, sh))) {
+        } else if (!(fast && [&] {
+                       int32_t ex[3];
+                       box_exits(w, R.s, sh, par.mask, ex);
+                       return skip_box(R, ex);
+                   }())) {
             if (STATS && fast) st.skip_out++;
             // step through the cell without lookups (budget ends inside it, or not exact)
             const uint32_t c[3] = {w[0], w[1], w[2]};
