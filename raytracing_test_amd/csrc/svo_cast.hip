@@ -70,6 +70,9 @@ struct CastParams {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
+#ifndef SVO_BRICK_BOX
+#define SVO_BRICK_BOX 0  // box crossing inside bricks too (A/B)
+#endif
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -399,7 +402,22 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                     done = true;
                     break;
                 }
+#if SVO_BRICK_BOX
+                if (fast) {
+                    // cross the forward box of empty voxels of this brick in one move
+                    int32_t ex[3];
+                    box_exits(w, R.s, 0u, bmask, ex);
+                    if (!skip_box(R, ex)) {
+                        while (R.steps > 0) dda_step(R);  // the budget ends inside the empty box
+                        done = true;
+                        break;
+                    }
+                } else {
+                    dda_step(R);
+                }
+#else
                 dda_step(R);
+#endif
                 if (STATS) st.brick_steps++;
                 wrap3(R, wm, w);
                 if (!same_cell(w, c, 2u)) break;
