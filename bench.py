@@ -43,11 +43,11 @@ def frame_origin(f):
     return (ORIGIN[0] + 64.0 * f, ORIGIN[1], ORIGIN[2] + 64.0 * f)
 
 
-def load_bray():
+def load_bray(config="c3"):
     p = os.path.join(ROOT, "profiles", "bray.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        c = d.get("C3")
+        c = d.get(config.upper())
         if c:
             return c["e_child_per_ray"], d
     return None, None
@@ -103,7 +103,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--cols", type=int, default=COLS)
+    ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
+                    help="c3: depth-12 / 1080p (the metric); c5: depth-14 (16384^2 columns, 7 levels) / 3840x2160")
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
@@ -127,6 +129,12 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
+    global LEVELS, W, H
+    if args.config == "c5":
+        LEVELS, W, H = 7, 3840, 2160
+        args.no_cpu_baseline = True  # the reference-format CPU tree of 16384^2 terrain exceeds its 2^32-byte pools
+    if args.cols is None:
+        args.cols = 4096 if args.config == "c3" else 16384
     t0 = time.time()
     tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
     build_s = time.time() - t0
@@ -226,12 +234,12 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    e_child, bray_meta = load_bray()
+    e_child, bray_meta = load_bray(args.config)
     roof = None
     if e_child is not None:
         b_ray = 16.0 * (e_child + 1.0) + 4.0 * e_child + B_OUT
         achieved = b_ray * rays_per_launch / avg_kernel_s / 1e9
-        traffic, _ = load_traffic()
+        traffic, _ = load_traffic() if args.config == "c3" else (None, None)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_ray": round(b_ray, 2), "avg_launch_ms": round(avg_kernel_s * 1e3, 4)}
@@ -252,8 +260,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols),
-        "config": {"ao_samples": args.ao, "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") + "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080 primary rays per GPU per "
-                               "step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % (args.cols, STEPS),
+        "config": {"ao_samples": args.ao, "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") +
+                   ("C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080" % args.cols if args.config == "c3" else
+                    "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols) +
+                   " primary rays per GPU per step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % STEPS,
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
                    "gather": world > 1 and not args.no_gather, "tree_nodes": info.n_nodes,
                    "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 2)},

@@ -75,6 +75,8 @@ int svo_get_block(const svo_world* w, int32_t x, int32_t y, int32_t z, svo_block
 int svo_delete_block(svo_world* w, int32_t x, int32_t y, int32_t z, int32_t level, svo_block* removed);
 /* genWorld (world_gen.cpp:13-42) over width x length columns (reference: 200 x 200) */
 int svo_gen_world(svo_world* w, int32_t width, int32_t length);
+/* genWorld's column puts (world_gen.cpp:24-39) from caller-given tops heights[x*length + z] */
+int svo_gen_heightfield(svo_world* w, int32_t width, int32_t length, const int32_t* heights);
 /* number of putBlock-visible tree nodes (diagnostics) */
 int svo_world_node_count(const svo_world* w, uint64_t* nodes);
 /* batched getBlock over n positions (xyz = 3 x int32 each) — the traverseTree batch lookup of
@@ -105,6 +107,9 @@ int svo_build(const svo_world* w, svo_tree** out);
 /* Build the same tree straight from genWorld's column formula over width x length columns
    (no per-voxel putBlock: depth-12 / depth-14 terrain); nthreads host threads (0 = all). */
 int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out);
+/* the same builder from caller-given column tops heights[x*length + z] (0 <= h <= extent-2) */
+int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t nthreads,
+                          svo_tree** out);
 int svo_tree_get_info(const svo_tree* t, svo_tree_info* out);
 /* palette entry `id` (id 0 = empty block) */
 int svo_tree_palette(const svo_tree* t, uint32_t id, svo_block* out);

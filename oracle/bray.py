@@ -29,6 +29,13 @@ def main():
     e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, nthreads=8) / (1920 * 1080)
     res["C3"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
                  "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
+    # C5: 7 levels, 3840x2160 from the same pose; every ray lands within ~2,600 voxels of the camera,
+    # so the oracle tree over the first 4096^2 columns of the 16384^2 terrain sees exactly the same
+    # voxels (a full 16384^2 reference-format tree would exceed the 2^32-byte pools)
+    t = O.Tree.terrain(7, 4096, 4096)
+    e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 3840, 2160, 16384, nthreads=8) / (3840 * 2160)
+    res["C5"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
+                 "tree": "depth-14 (7 levels), first 4096^2 columns, reference node/array format, uniform regions collapsed"}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "profiles", "bray.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -610,13 +610,13 @@ static void o_cbuild(ocbuild* B, uint32_t node, int x0, int y0, int z0, int s) {
     }
 }
 
-/* terrain only (no initTetraHexaTree debug puts); needs W, L <= extent and 1 <= h, max(h,20) < extent */
+/* terrain only (no initTetraHexaTree debug puts); needs W, L <= extent and 0 <= h, max(h,20) < extent-1 */
 EXPORT int orc_build_terrain_collapsed(otree* t, const int32_t* heights, int W, int L) {
     int levels = t->max_depth - 1;
     int E = 1 << (2 * levels);
     if (W > E || L > E) return -1;
     for (size_t i = 0; i < (size_t)W * L; i++)
-        if (heights[i] < 1 || heights[i] >= E - 1 || 21 >= E) return -2;
+        if (heights[i] < 0 || heights[i] >= E - 1 || 21 >= E) return -2;
     orc_init_clean_root(t);
     ocbuild B;
     B.t = t;

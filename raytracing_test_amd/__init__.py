@@ -109,7 +109,8 @@ ABI_SYMBOLS = (
     "svo_build_terrain", "svo_tree_get_info", "svo_tree_palette", "svo_tree_get_block", "svo_tree_export",
     "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
-    "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere",
+    "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
+    "svo_build_heightfield",
 )
 
 
@@ -163,6 +164,8 @@ def lib():
     L.svo_noise2.argtypes = [C.c_int64, vp, vp, C.c_int64, vp]
     L.svo_terrain_heights.argtypes = [i32, i32, i32, vp]
     L.svo_hemisphere.argtypes = [i32, vp]
+    L.svo_gen_heightfield.argtypes = [vp, i32, i32, vp]
+    L.svo_build_heightfield.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
     _lib = L
     return L
 
@@ -298,6 +301,11 @@ class World:
     def gen_world(self, width=200, length=200):
         _check(lib().svo_gen_world(self._h, width, length), "svo_gen_world")
 
+    def gen_heightfield(self, heights):
+        """genWorld's column puts from given column tops, heights shape (width, length)"""
+        h = np.ascontiguousarray(heights, np.int32)
+        _check(lib().svo_gen_heightfield(self._h, h.shape[0], h.shape[1], h.ctypes.data_as(C.c_void_p)), "svo_gen_heightfield")
+
     def node_count(self):
         n = C.c_uint64()
         _check(lib().svo_world_node_count(self._h, C.byref(n)), "svo_world_node_count")
@@ -333,6 +341,15 @@ class Tree:
         h = C.c_void_p()
         _check(lib().svo_build_terrain(levels, width, length, nthreads, C.byref(h)), "svo_build_terrain")
         return cls(h)
+
+    @classmethod
+    def heightfield(cls, levels, heights, nthreads=0):
+        """the terrain builder on given column tops, heights shape (width, length)"""
+        h = np.ascontiguousarray(heights, np.int32)
+        t = C.c_void_p()
+        _check(lib().svo_build_heightfield(levels, h.shape[0], h.shape[1], h.ctypes.data_as(C.c_void_p), nthreads, C.byref(t)),
+               "svo_build_heightfield")
+        return cls(t)
 
     def info(self):
         i = TreeInfo()

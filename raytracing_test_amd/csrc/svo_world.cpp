@@ -302,6 +302,9 @@ struct TerrainIds {
 };
 }  // namespace
 
+// genWorld's column puts (world_gen.cpp:24-39) for one column with top y
+static void gen_column(svo_world* w, int32_t x, int32_t z, int32_t y);
+
 // genWorld (world_gen.cpp:13-42) over width x length columns
 extern "C" int svo_gen_world(svo_world* w, int32_t width, int32_t length) {
     if (!w || width < 0 || length < 0) SVO_FAIL(SVO_EINVAL, "svo_gen_world: bad argument");
@@ -309,25 +312,33 @@ extern "C" int svo_gen_world(svo_world* w, int32_t width, int32_t length) {
     simplex2_seed(n42, 42);
     simplex2_seed(n64, 64);
     simplex2_seed(n100, 100);
+    for (int32_t x = 0; x < width; x++)
+        for (int32_t z = 0; z < length; z++) gen_column(w, x, z, terrain_height(n42.perm, n64.perm, n100.perm, x, z));
+    return SVO_OK;
+}
+
+// the same puts from caller-given column tops heights[x*length + z]
+extern "C" int svo_gen_heightfield(svo_world* w, int32_t width, int32_t length, const int32_t* heights) {
+    if (!w || width < 0 || length < 0 || (!heights && (int64_t)width * length > 0)) SVO_FAIL(SVO_EINVAL, "svo_gen_heightfield: bad argument");
+    for (int32_t x = 0; x < width; x++)
+        for (int32_t z = 0; z < length; z++) gen_column(w, x, z, heights[(size_t)x * length + z]);
+    return SVO_OK;
+}
+
+static void gen_column(svo_world* w, int32_t x, int32_t z, int32_t y) {
     const uint64_t green = rgb_to_u64(0, 150, 10), brown = rgb_to_u64(45, 18, 0), grey = rgb_to_u64(33, 33, 33);
     const int32_t voxel = w->levels + 1;
     auto id = [&](uint32_t f, uint64_t c) { return (uint16_t)w->pal.intern(Material{1u | f, c, 0.0f}); };
-    for (int32_t x = 0; x < width; x++) {
-        for (int32_t z = 0; z < length; z++) {
-            int32_t y = terrain_height(n42.perm, n64.perm, n100.perm, x, z);
-            if (y < 20) {
-                uint16_t water = id(0x4u | 0x10u, green);
-                for (int32_t i = 20; i > y; i--) put_block_id(w, x, i, z, water, voxel);
-                put_block_id(w, x, y, z, id(0, brown), voxel);
-            } else {
-                put_block_id(w, x, y, z, id(0, green), voxel);
-            }
-            y--;
-            for (int i = 3; y > 0 && i; i--, y--) put_block_id(w, x, y, z, id(0, brown), voxel);
-            for (; y > 0; y--) put_block_id(w, x, y, z, id(0, grey), voxel);
-        }
+    if (y < 20) {
+        const uint16_t water = id(0x4u | 0x10u, green);
+        for (int32_t i = 20; i > y; i--) put_block_id(w, x, i, z, water, voxel);
+        put_block_id(w, x, y, z, id(0, brown), voxel);
+    } else {
+        put_block_id(w, x, y, z, id(0, green), voxel);
     }
-    return SVO_OK;
+    y--;
+    for (int i = 3; y > 0 && i; i--, y--) put_block_id(w, x, y, z, id(0, brown), voxel);
+    for (; y > 0; y--) put_block_id(w, x, y, z, id(0, grey), voxel);
 }
 
 // ================================================================================================
@@ -512,34 +523,58 @@ struct Region {
 };
 }  // namespace
 
+static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, std::vector<int16_t>& hg,
+                              svo_tree** out);
+
 extern "C" int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out) {
     if (!out) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: out is NULL");
     if (levels < 2 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: levels must be in [2, 7]");
     const int32_t E = 1 << (2 * levels);
     if (width < 1 || length < 1 || width > E || length > E) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: columns must fit the extent");
+    // heights (world_gen.cpp:22), parallel over x
+    std::vector<int16_t> hg((size_t)width * length);
+    Simplex2 n42, n64, n100;
+    simplex2_seed(n42, 42);
+    simplex2_seed(n64, 64);
+    simplex2_seed(n100, 100);
+    std::atomic<int> bad(0);
+    parallel_for(width, nthreads, [&](int64_t b, int64_t e) {
+        for (int64_t x = b; x < e; x++)
+            for (int32_t z = 0; z < length; z++) {
+                int32_t h = terrain_height(n42.perm, n64.perm, n100.perm, (int32_t)x, z);
+                if (h < 0 || h > 32767) bad = 1;
+                hg[(size_t)x * length + z] = (int16_t)h;
+            }
+    });
+    if (bad) SVO_FAIL(SVO_ERANGE, "svo_build_terrain: a column top falls outside [0, 32767]");
+    return build_from_heights(levels, width, length, nthreads, hg, out);
+}
+
+extern "C" int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t nthreads,
+                                     svo_tree** out) {
+    if (!out || !heights) SVO_FAIL(SVO_EINVAL, "svo_build_heightfield: NULL argument");
+    if (levels < 2 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_build_heightfield: levels must be in [2, 7]");
+    const int32_t E = 1 << (2 * levels);
+    if (width < 1 || length < 1 || width > E || length > E) SVO_FAIL(SVO_EINVAL, "svo_build_heightfield: columns must fit the extent");
+    std::vector<int16_t> hg((size_t)width * length);
+    for (size_t i = 0; i < hg.size(); i++) {
+        if (heights[i] < 0 || heights[i] > 32767) SVO_FAIL(SVO_ERANGE, "svo_build_heightfield: heights must be in [0, extent-2]");
+        hg[i] = (int16_t)heights[i];
+    }
+    return build_from_heights(levels, width, length, nthreads, hg, out);
+}
+
+static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, std::vector<int16_t>& hg,
+                              svo_tree** out) {
+    const int32_t E = 1 << (2 * levels);
+    for (size_t i = 0; i < hg.size(); i++)
+        if (hg[i] + 1 >= E || 21 >= E)
+            SVO_FAIL(SVO_ERANGE, "svo_build_terrain: a column top falls outside [0, extent-2] (wrap not supported here; use svo_gen_world)");
     TerrainCtx T;
     T.levels = levels;
     T.E = E;
     T.W = width;
     T.L = length;
-    // ---- heights (world_gen.cpp:22), parallel over x
-    std::vector<int16_t> hg((size_t)width * length);
-    {
-        Simplex2 n42, n64, n100;
-        simplex2_seed(n42, 42);
-        simplex2_seed(n64, 64);
-        simplex2_seed(n100, 100);
-        std::atomic<int> bad(0);
-        parallel_for(width, nthreads, [&](int64_t b, int64_t e) {
-            for (int64_t x = b; x < e; x++)
-                for (int32_t z = 0; z < length; z++) {
-                    int32_t h = terrain_height(n42.perm, n64.perm, n100.perm, (int32_t)x, z);
-                    if (h < 1 || h + 1 >= E || 21 >= E || h > 32767) bad = 1;
-                    hg[(size_t)x * length + z] = (int16_t)h;
-                }
-        });
-        if (bad) SVO_FAIL(SVO_ERANGE, "svo_build_terrain: a column top falls outside [1, extent-2] (wrap not supported here; use svo_gen_world)");
-    }
     T.h = hg.data();
     // ---- min/max pyramid over aligned 4^k footprints
     T.pyr.W = width;

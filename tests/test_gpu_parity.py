@@ -291,3 +291,22 @@ def test_ao_depth12_sampled(rt, oracle_mod, depth12):
     ao, hit = T.cast_frame_ao((4, 90, 4), dn, 1920, 1080, 16384, 16, 5, pixels=pix, nthreads=16)
     assert np.array_equal(out["ao"][pix], ao)
     assert out["ao"].mean() > 0.5  # terrain occludes part of the hemisphere
+
+
+def test_depth14_4k_sampled_parity(rt, oracle_mod, torch_cuda):
+    """C5: depth-14 (16384^2 columns, 7 levels), 3840x2160 from the C1 pose; sampled pixels against the
+    oracle's 7-level reference-format tree over the first 4096^2 columns (every ray of this pose lands
+    within ~2,600 voxels; the full reference-format tree would exceed its 2^32-byte pools)."""
+    t = rt.Tree.terrain(7, 16384, 16384, nthreads=16).upload(0)
+    T = oracle_mod.Tree.terrain(7, 4096, 4096, nthreads=16)
+    dn = rt.normalize([1, -0.45, 1])
+    W, H = 3840, 2160
+    out = rt.decode_hits(t.cast_frame((4, 90, 4), dn, W, H, 16384))
+    pix = np.random.default_rng(14).integers(0, W * H, 4000)
+    ref = T.cast_frame((4, 90, 4), dn, W, H, 16384, pixels=pix, nthreads=16)
+    assert ref["rc"] == 0
+    assert np.array_equal(out["pos"][pix], ref["pos"]) and np.array_equal(out["steps"][pix], ref["steps"])
+    assert np.array_equal(out["hit"][pix], ref["hit"] != 0)
+    assert np.array_equal(out["t"][pix], ref["t"].astype(np.float32))
+    assert np.abs(out["pos"][:, [0, 2]]).max() < 4096  # the premise of the 4096^2 oracle
+    del t

@@ -153,3 +153,22 @@ def test_hemisphere_table_matches_reference_generator(rt, oracle_mod):
     # N = 16 (BASELINE config C4): same formula; the reference only ships N = 20 (parity via formula)
     for n in (1, 8, 16, 32, 64):
         assert np.array_equal(rt.hemisphere(n).view(np.uint32), oracle_mod.hemisphere(n).view(np.uint32)), n
+
+
+def test_heightfield_builders_agree_on_adversarial_heights(rt):
+    """column tops 0 (dirt at y = 0 under water), 1..3 (short dirt runs), exactly 20, aligned steps
+    and partial footprints: the column builder must equal per-voxel putBlock node for node"""
+    rng = np.random.default_rng(17)
+    for levels, W, L in ((4, 64, 64), (4, 130, 77), (5, 256, 256)):
+        h = rng.integers(0, 40, (W, L)).astype(np.int32)
+        h[::7, :] = 0
+        h[:, ::5] = 20
+        h[10:30, 10:30] = 19
+        h[40:48, 0:16] = 3  # a flat aligned plateau: uniform dirt bricks
+        w = rt.World(levels)
+        w.gen_heightfield(h)
+        a, b = w.build(), rt.Tree.heightfield(levels, h)
+        na, ma = a.export()
+        nb, mb = b.export()
+        assert a.palette() == b.palette()
+        assert np.array_equal(na, nb) and np.array_equal(ma, mb), (levels, W, L)
