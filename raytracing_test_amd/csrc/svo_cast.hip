@@ -241,6 +241,8 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 
 struct Stats {
     uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
+    uint32_t skip_by_sh[4];  // crossings whose box is made of 2^sh cells: sh = 2, 4, 6, >= 8
+    uint32_t bricks;         // brick visits
 };
 
 // wave-wide max / sum (diagnostics only)
@@ -368,7 +370,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0};
     Parent par;
     par.valid = false;
     par.mask = 0ull;
@@ -388,6 +390,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             mat = binfo >> 16;
             done = true;
         } else if (kind == R_BRICK) {
+            if (STATS) st.bricks++;
             // voxel steps inside the brick, solid mask in registers
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
@@ -445,6 +448,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             done = !left;
         } else if (STATS) {
             st.skips++;
+            st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
         }
     }
     if (STATS) {
@@ -462,6 +466,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         atomicAdd(P.stats + 4, (unsigned long long)st.skip_out);
         atomicAdd(P.stats + 5, (unsigned long long)st.brick_steps);
         atomicAdd(P.stats + 6, (unsigned long long)st.plain_steps);
+        for (int k = 0; k < 4; k++) atomicAdd(P.stats + 9 + k, (unsigned long long)st.skip_by_sh[k]);
+        atomicAdd(P.stats + 13, (unsigned long long)st.bricks);
     }
     Hit h;
     h.x = R.r[0];
