@@ -73,6 +73,9 @@ constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
 #ifndef SVO_BRICK_BOX
 #define SVO_BRICK_BOX 0  // box crossing inside bricks too (A/B)
 #endif
+#ifndef SVO_A_F64
+#define SVO_A_F64 0  // keep absDelta in f64 registers (A/B)
+#endif
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -129,13 +132,21 @@ __device__ __forceinline__ int32_t count_before(double T, double a, float inva, 
 struct Ray {
     int32_t r[3];   // current voxel (unwrapped)
     double T[3];    // next crossing per axis (deltaPos)
+#if SVO_A_F64
+    double ad[3];   // absDelta
+#else
     float af[3];    // absDelta: an f32 value widened to f64 by the reference (ray_caster.cpp:35-41)
+#endif
     float ia[3];    // 1/absDelta estimate (counts only)
     int32_t s[3];   // step
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
     float tlast;    // crossing value of the last step, as output (f32)
+#if SVO_A_F64
+    __device__ __forceinline__ double a(int k) const { return ad[k]; }
+#else
     __device__ __forceinline__ double a(int k) const { return (double)af[k]; }
+#endif
 };
 
 // one DDA step (ray_caster.cpp:70-80), branch-free
@@ -358,7 +369,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         const Dda1 ax = dda_axis(o[k], d[k]);
         R.r[k] = ax.cell;
         R.T[k] = ax.dpos;
+#if SVO_A_F64
+        R.ad[k] = ax.adelta;
+#else
         R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
+#endif
         R.s[k] = ax.step;
         R.ia[k] = (float)(1.0 / ax.adelta);
     }
