@@ -137,7 +137,6 @@ struct Ray {
 #else
     float af[3];    // absDelta: an f32 value widened to f64 by the reference (ray_caster.cpp:35-41)
 #endif
-    float ia[3];    // 1/absDelta estimate (counts only)
     int32_t s[3];   // step
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
@@ -234,7 +233,8 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         // axis k's events tied with V come after the exit event when rank_k > rank_b (k < b)
-        const int32_t c = count_before(R.T[k], R.a(k), R.ia[k], V, (uint32_t)k < b);
+        // 1/absDelta estimate, recomputed (an f32 reciprocal is one instruction; a register is not)
+        const int32_t c = count_before(R.T[k], R.a(k), __builtin_amdgcn_rcpf((float)R.a(k)), V, (uint32_t)k < b);
         n[k] = (uint32_t)k == b ? e[k] : c;
         total += n[k];
     }
@@ -375,7 +375,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
 #endif
         R.s[k] = ax.step;
-        R.ia[k] = (float)(1.0 / ax.adelta);
     }
     R.steps = budget;
     R.axis = 3u;
