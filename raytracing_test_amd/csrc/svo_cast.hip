@@ -495,9 +495,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     return h;
 }
 
-template <bool STATS, bool STAMPS>
+template <bool STATS, bool STAMPS, bool AO>
 #ifndef SVO_MIN_WAVES
-#define SVO_MIN_WAVES 6  // 80 VGPRs: 6 waves per SIMD without spills
+// primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
+// ~80 (6 waves)
+#define SVO_MIN_WAVES ((AO || STATS) ? 6 : 8)
 #endif
 __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams P) {
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -511,7 +513,8 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
     // hemisphere AO sample set, broadcast from LDS
     __shared__ float ao_tab[3 * 64];
-    for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
+    if (AO)
+        for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
     int64_t blk = blockIdx.x;
     if (P.flags & SVO_CAST_XCD_SWIZZLE) {
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
-        if (P.ao_n > 0) {
+        if (AO) {
             // AO rays from the centre of lastPos, pole turned to the hit face's normal (A8)
             uint32_t cnt = 0u;
             if (h.info & HIT_BIT) {
@@ -720,12 +723,18 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
-    if (P.flags & SVO_CAST_STATS)
-        hipLaunchKernelGGL((k_cast<true, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-    else if (P.flags & SVO_CAST_TIMELINE)
-        hipLaunchKernelGGL((k_cast<false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
-    else
-        hipLaunchKernelGGL((k_cast<false, false>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    const dim3 grid((uint32_t)blocks), block(kBlock);
+    hipStream_t st = (hipStream_t)stream;
+    if (P.ao_n > 0) {
+        if (P.flags & SVO_CAST_STATS) hipLaunchKernelGGL((k_cast<true, true, true>), grid, block, 0, st, P);
+        else hipLaunchKernelGGL((k_cast<false, false, true>), grid, block, 0, st, P);
+    } else if (P.flags & SVO_CAST_STATS) {
+        hipLaunchKernelGGL((k_cast<true, true, false>), grid, block, 0, st, P);
+    } else if (P.flags & SVO_CAST_TIMELINE) {
+        hipLaunchKernelGGL((k_cast<false, true, false>), grid, block, 0, st, P);
+    } else {
+        hipLaunchKernelGGL((k_cast<false, false, false>), grid, block, 0, st, P);
+    }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -754,7 +763,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL((k_cast<false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL((k_cast<false, false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
