@@ -70,6 +70,9 @@ struct CastParams {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
+#ifndef SVO_SKIP3
+#define SVO_SKIP3 1
+#endif
 #ifndef SVO_BRICK_BOX
 #define SVO_BRICK_BOX 0  // box crossing inside bricks too (A/B)
 #endif
@@ -113,20 +116,6 @@ __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
     const int u = min(dbl_lsb(T), dbl_lsb(a));
     const double bound = __builtin_fabs(T) + (double)(budget + 2) * a;
     return dbl_ilogb(bound) + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
-}
-
-// Number of events j >= 0 of the sequence T + j*a that come before an event of value V on another
-// axis: those with T + j*a < V (strict: this axis loses ties) or <= V.  Exact under exact_axis:
-// q = (V-T)/a is estimated to within 1 (f32 reciprocal, relative error < 2^-22), k0 = trunc(q),
-// and the exact remainder r0 = V - (T + k0*a) (all terms on the ray's 2^lsb grid, below
-// 2^(lsb+53)) settles k0, k0+1 or k0+2.  Counts above the budget may be off; the caller then
-// rejects the move anyway (total > steps).  Branch-free.
-__device__ __forceinline__ int32_t count_before(double T, double a, float inva, double V, bool strict) {
-    const double q = (V - T) * (double)inva;
-    const int32_t k0 = q > 0.0 ? (int32_t)q : 0;
-    const double r0 = V - (T + (double)k0 * a);
-    const int32_t k = k0 + (strict ? (int32_t)(r0 > 0.0) + (int32_t)(r0 > a) : (int32_t)(r0 >= 0.0) + (int32_t)(r0 >= a));
-    return k;
 }
 
 struct Ray {
@@ -214,6 +203,19 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
 // leave the box.  Returns false (state unchanged) when the budget ends inside the box.
+// #{ j >= 0 : T + j*a < W }, exact under exact_axis.  k0 = trunc((W-T)/a) from an f32 estimate (error < 1 for counts below 2^20) is at
+// most 2 below the count; the monotone tests T + k0*a < W and T + (k0+1)*a < W (both values exact
+// on the ray's grid) add the rest.
+__device__ __forceinline__ int32_t count_lt_w(double T, double a, double W) {
+    const float q = (float)(W - T) * __builtin_amdgcn_rcpf((float)a);
+    const int32_t k0 = (int32_t)fmaxf(q, 0.0f);
+    const double X = T + (double)k0 * a;
+    const double X1 = X + a;
+    return k0 + (int32_t)(X < W) + (int32_t)(X1 < W);
+}
+
+// Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
+// leave the box.  Returns false (state unchanged) when the budget ends inside the box.
 __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     const int32_t lim = R.steps + 1;  // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
@@ -226,26 +228,49 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
     const bool by = !bx && (E[1] < E[2]);
-    const uint32_t b = bx ? 0u : (by ? 1u : 2u);
+    const bool bz = !bx && !by;
     const double V = bx ? E[0] : (by ? E[1] : E[2]);
-    int32_t n[3];
-    int32_t total = 0;
+    // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
+    // (rank_k > rank_b, i.e. k < b), else T + j*a <= V, which on doubles is < nextup(V).
+    const uint64_t vb = (uint64_t)__double_as_longlong(V);
+    const double Vn = V > 0.0 ? __longlong_as_double((long long)(vb + 1u))
+                              : (V < 0.0 ? __longlong_as_double((long long)(vb - 1u)) : __longlong_as_double(1ll));
+#if SVO_SKIP3
+    // every axis through the same count: the exit axis b counts to exactly e_b against nextup(V)
+    int32_t total = 0, n[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        // axis k's events tied with V come after the exit event when rank_k > rank_b (k < b)
-        // 1/absDelta estimate, recomputed (an f32 reciprocal is one instruction; a register is not)
-        const int32_t c = count_before(R.T[k], R.a(k), __builtin_amdgcn_rcpf((float)R.a(k)), V, (uint32_t)k < b);
-        n[k] = (uint32_t)k == b ? e[k] : c;
+        const bool strict = bx ? false : (by ? k == 0 : k != 2);
+        n[k] = count_lt_w(R.T[k], R.a(k), strict ? V : Vn);
         total += n[k];
     }
     if (total > R.steps) return false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        R.r[k] += R.s[k] * n[k];
         R.T[k] += (double)n[k] * R.a(k);
+        R.r[k] += R.s[k] * n[k];
     }
+#else
+    // the two other axes: p = (x exits ? y : x), q = (z exits ? y : z)
+    const double Tp = bx ? R.T[1] : R.T[0], ap = bx ? R.a(1) : R.a(0);
+    const double Tq = bz ? R.T[1] : R.T[2], aq = bz ? R.a(1) : R.a(2);
+    const int32_t cp = count_lt_w(Tp, ap, bx ? Vn : V);  // p is x (strict) unless x exits
+    const int32_t cq = count_lt_w(Tq, aq, bz ? V : Vn);  // q is z (non-strict) unless z exits
+    const int32_t eb = bx ? e[0] : (by ? e[1] : e[2]);
+    const int32_t total = eb + cp + cq;
+    if (total > R.steps) return false;
+    const int32_t n0 = bx ? eb : cp;
+    const int32_t n1 = bx ? cp : (by ? eb : cq);
+    const int32_t n2 = bz ? eb : cq;
+    R.T[0] += (double)n0 * R.a(0);
+    R.T[1] += (double)n1 * R.a(1);
+    R.T[2] += (double)n2 * R.a(2);
+    R.r[0] += R.s[0] * n0;
+    R.r[1] += R.s[1] * n1;
+    R.r[2] += R.s[2] * n2;
+#endif
     R.tlast = (float)V;
-    R.axis = b;
+    R.axis = bx ? 0u : (by ? 1u : 2u);
     R.steps -= total;
     return true;
 }
