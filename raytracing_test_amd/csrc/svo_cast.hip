@@ -159,45 +159,50 @@ __device__ __forceinline__ int32_t exit_steps(uint32_t w, int32_t s, uint32_t sh
     return s > 0 ? (int32_t)(lo + (1u << sh) - w) : (int32_t)(w - lo + 1u);
 }
 
+// Run of free slots (4-slot line, bit = occupied) from slot c in the step direction: the last free
+// slot above c (s > 0) or below c (s < 0).  Branch-free.
+__device__ __forceinline__ uint32_t run_hi(uint32_t occ, uint32_t c) {
+    return c + (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
+}
+__device__ __forceinline__ uint32_t run_lo(uint32_t occ, uint32_t c) {
+    return 32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u)));  // one above the nearest occupied slot below
+}
+
 // Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
 // the run along x from the mask row, then whole rows along z, then whole planes along y), all from
-// the parent's 64-bit child mask in registers.  Returns per-axis steps to leave the box.
+// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
 __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, int32_t e[3]) {
     const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
+    const uint32_t lo = (uint32_t)pmask, hi = (uint32_t)(pmask >> 32);
     // x run through the row (cy, cz)
     const uint32_t row = (uint32_t)(pmask >> (16u * cz + 4u * cy)) & 0xFu;
-    uint32_t x0, x1;
-    if (s[0] > 0) {
-        const uint32_t n = (uint32_t)__builtin_ctz((row >> cx) | (1u << (4u - cx)));
-        x0 = cx;
-        x1 = cx + n - 1u;
-    } else {
-        const uint32_t below = row & ((1u << cx) - 1u);  // occupied slots below cx
-        x0 = below ? (32u - (uint32_t)__builtin_clz(below)) : 0u;
-        x1 = cx;
-    }
-    const uint32_t xm = ((1u << (x1 + 1u)) - 1u) & ~((1u << x0) - 1u);
-    // whole rows along z
-    uint32_t z0 = cz, z1 = cz;
-    if (s[2] > 0) {
-        while (z1 < 3u && !((uint32_t)(pmask >> (16u * (z1 + 1u) + 4u * cy)) & xm)) z1++;
-    } else {
-        while (z0 > 0u && !((uint32_t)(pmask >> (16u * (z0 - 1u) + 4u * cy)) & xm)) z0--;
-    }
-    // whole planes (x range x z range) along y
-    uint64_t plane = 0ull;
-    for (uint32_t z = z0; z <= z1; z++) plane |= (uint64_t)xm << (16u * z);
-    uint32_t y0 = cy, y1 = cy;
-    if (s[1] > 0) {
-        while (y1 < 3u && !(pmask & (plane << (4u * (y1 + 1u))))) y1++;
-    } else {
-        while (y0 > 0u && !(pmask & (plane << (4u * (y0 - 1u))))) y0--;
-    }
-    const uint32_t lo[3] = {x0, y0, z0}, hi[3] = {x1, y1, z1};
+    const uint32_t x0 = s[0] > 0 ? cx : run_lo(row, cx);
+    const uint32_t x1 = s[0] > 0 ? run_hi(row, cx) : cx;
+    const uint32_t xm = ((2u << x1) - 1u) & ~((1u << x0) - 1u);
+    // rows (cy, z) over the x run: bit z of zocc = the row holds a solid slot
+    const uint32_t xm2 = (xm | (xm << 16)) << (4u * cy);
+    const uint32_t tl = lo & xm2, th = hi & xm2;
+    const uint32_t zocc = (uint32_t)((tl & 0xFFFFu) != 0u) | ((uint32_t)(tl > 0xFFFFu) << 1) |
+                          ((uint32_t)((th & 0xFFFFu) != 0u) << 2) | ((uint32_t)(th > 0xFFFFu) << 3);
+    const uint32_t z0 = s[2] > 0 ? cz : run_lo(zocc, cz);
+    const uint32_t z1 = s[2] > 0 ? run_hi(zocc, cz) : cz;
+    const uint32_t zm = ((2u << z1) - 1u) & ~((1u << z0) - 1u);
+    // planes y over the x run x z run: bit y of yocc = the plane holds a solid slot
+    const uint32_t xrep = xm * 0x1111u;
+    const uint32_t pl = ((zm & 1u) ? xrep : 0u) | ((zm & 2u) ? xrep << 16 : 0u);
+    const uint32_t ph = ((zm & 4u) ? xrep : 0u) | ((zm & 8u) ? xrep << 16 : 0u);
+    uint32_t q = (lo & pl) | (hi & ph);
+    q = (q | (q >> 16)) & 0xFFFFu;
+    q |= q >> 1;
+    q |= q >> 2;
+    const uint32_t yocc = (q & 1u) | ((q >> 3) & 2u) | ((q >> 6) & 4u) | ((q >> 9) & 8u);
+    const uint32_t y0 = s[1] > 0 ? cy : run_lo(yocc, cy);
+    const uint32_t y1 = s[1] > 0 ? run_hi(yocc, cy) : cy;
+    const uint32_t lo3[3] = {x0, y0, z0}, hi3[3] = {x1, y1, z1};
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const uint32_t base = (w[k] >> (sh + 2u)) << (sh + 2u);
-        e[k] = s[k] > 0 ? (int32_t)(base + ((hi[k] + 1u) << sh) - w[k]) : (int32_t)(w[k] - (base + (lo[k] << sh)) + 1u);
+        e[k] = s[k] > 0 ? (int32_t)(base + ((hi3[k] + 1u) << sh) - w[k]) : (int32_t)(w[k] - (base + (lo3[k] << sh)) + 1u);
     }
 }
 
