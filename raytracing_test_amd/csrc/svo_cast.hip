@@ -70,6 +70,9 @@ struct CastParams {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
+#ifndef SVO_FMA
+#define SVO_FMA 1
+#endif
 #ifndef SVO_SKIP3
 #define SVO_SKIP3 1
 #endif
@@ -136,6 +139,15 @@ struct Ray {
     __device__ __forceinline__ double a(int k) const { return (double)af[k]; }
 #endif
 };
+
+// T + k*a for a fast ray: exact (exact_axis), so one fused operation gives the same double
+__device__ __forceinline__ double on_grid(double T, int32_t k, double a) {
+#if SVO_FMA
+    return __builtin_fma((double)k, a, T);
+#else
+    return T + (double)k * a;
+#endif
+}
 
 // one DDA step (ray_caster.cpp:70-80), branch-free
 __device__ __forceinline__ void dda_step(Ray& R) {
@@ -214,7 +226,7 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 __device__ __forceinline__ int32_t count_lt_w(double T, double a, double W) {
     const float q = (float)(W - T) * __builtin_amdgcn_rcpf((float)a);
     const int32_t k0 = (int32_t)fmaxf(q, 0.0f);
-    const double X = T + (double)k0 * a;
+    const double X = on_grid(T, k0, a);
     const double X1 = X + a;
     return k0 + (int32_t)(X < W) + (int32_t)(X1 < W);
 }
@@ -228,7 +240,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         e[k] = min(ex[k], lim);
-        E[k] = R.T[k] + (double)(e[k] - 1) * R.a(k);
+        E[k] = on_grid(R.T[k], e[k] - 1, R.a(k));
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
@@ -252,7 +264,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     if (total > R.steps) return false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        R.T[k] += (double)n[k] * R.a(k);
+        R.T[k] = on_grid(R.T[k], n[k], R.a(k));
         R.r[k] += R.s[k] * n[k];
     }
 #else
@@ -267,9 +279,9 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     const int32_t n0 = bx ? eb : cp;
     const int32_t n1 = bx ? cp : (by ? eb : cq);
     const int32_t n2 = bz ? eb : cq;
-    R.T[0] += (double)n0 * R.a(0);
-    R.T[1] += (double)n1 * R.a(1);
-    R.T[2] += (double)n2 * R.a(2);
+    R.T[0] = on_grid(R.T[0], n0, R.a(0));
+    R.T[1] = on_grid(R.T[1], n1, R.a(1));
+    R.T[2] = on_grid(R.T[2], n2, R.a(2));
     R.r[0] += R.s[0] * n0;
     R.r[1] += R.s[1] * n1;
     R.r[2] += R.s[2] * n2;
