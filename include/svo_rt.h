@@ -158,10 +158,14 @@ typedef struct {
     int32_t flags;     /* SVO_CAST_* bits, 0 = default */
     int32_t ao_samples; /* hemisphere AO rays per primary hit (0 = off, <= 64; reference: 20) */
     int32_t ao_steps;   /* DDA budget of each AO ray (reference: 5, light_scattering.frag:231) */
-    uint64_t* stats;   /* optional device u64[16] accumulating per-launch counters when
+    uint64_t* stats;   /* optional device u64[SVO_STATS_HEADER] accumulating per-launch counters when
                           flags & SVO_CAST_STATS: rays, lookups, node loads, cell skips,
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
-                          lane work units, wave-max work units x 64; then 2 stamps per block
+                          lane work units, wave-max work units x 64, crossings by box cell
+                          size (4 slots), brick visits, wave-level loop iterations,
+                          wave-level brick voxel steps, LDS node reads, lookups started at
+                          the root, lookups answered by the cached parent, wave-level
+                          crossings, wave-level descent levels; then 2 stamps per block
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
 
@@ -173,7 +177,8 @@ typedef struct {
 /* svo_cast_desc.flags, scheduling (results identical): frames are dispatched top tile row first
    (longest rays first); this bit restores bottom-first order */
 #define SVO_CAST_BOTTOM_FIRST 4
-/* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[16 + 2*block] only */
+/* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[SVO_STATS_HEADER + 2*block] only */
+#define SVO_STATS_HEADER 32
 #define SVO_CAST_TIMELINE 32
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
 #define SVO_CAST_XCD_SWIZZLE 16

@@ -70,6 +70,10 @@ struct CastParams {
 
 constexpr int kBlock = 256;
 constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
+constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
+#ifndef SVO_PEND8
+#define SVO_PEND8 0
+#endif
 #ifndef SVO_FMA
 #define SVO_FMA 1
 #endif
@@ -296,7 +300,17 @@ struct Stats {
     uint32_t lookups, loads, skips, skip_out, brick_steps, plain_steps;
     uint32_t skip_by_sh[4];  // crossings whose box is made of 2^sh cells: sh = 2, 4, 6, >= 8
     uint32_t bricks;         // brick visits
+    uint32_t wv_iters, wv_brick;  // wave-level executions (counted on the first active lane): outer
+                                  // loop iterations, brick voxel steps
+    uint32_t lds_reads, root_starts, cache_empty;  // LDS node reads; lookups started at the root;
+                                                   // lookups answered by the cached parent mask
+    uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
 };
+
+// true on one lane of the active lanes (wave-level counters)
+__device__ __forceinline__ bool wave_lead() {
+    return (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+}
 
 // wave-wide max / sum (diagnostics only)
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
@@ -338,24 +352,35 @@ __device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uin
 
 template <bool STATS>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                           uint32_t nlds, const uint32_t w[3], Parent& par, uint32_t& sh_out, uint64_t& bmask,
-                                           uint32_t& bref, uint32_t& binfo, Stats& st) {
+                                           uint32_t nlds, uint32_t* __restrict__ path, const uint32_t w[3], Parent& par,
+                                           uint32_t& sh_out, uint64_t& bmask, uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
-    if (par.valid && ((((w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2])) >> (par.sh + 2u)) == 0u)) {
+    const uint32_t diff = (w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2]);
+    if (par.valid && (diff >> (par.sh + 2u)) == 0u) {
         const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
         if (!((par.mask >> sl) & 1ull)) {
             sh_out = par.sh;
+            if (STATS) st.cache_empty++;
             return R_EMPTY;
         }
         ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
+    } else if (par.valid) {
+        // restart at the deepest node of the previous path whose region also holds this cell:
+        // depth levels-1-floor(h/2), h = highest bit in which the two positions differ
+        dd = P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1);
+        ni = path[dd * kBlock];
+    } else if (STATS) {
+        st.root_starts++;
     }
     for (; dd < P.levels; dd++) {
         Node n;
+        if (STATS) st.wv_descents += wave_lead();
         if (ni < nlds) {
             n = lds[ni];
+            if (STATS) st.lds_reads++;
         } else {
             n = load_node(rsrc, ni);
             if (STATS) st.loads++;
@@ -369,6 +394,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             return kind == K_SOLID ? R_SOLID : R_BRICK;
         }
         const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
+        path[dd * kBlock] = ni;
         par.mask = n.mask;
         par.ref = n.ref;
         par.sh = sh;
@@ -404,7 +430,7 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 // One ray with castRayFromCam semantics.
 template <bool STATS>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                     uint32_t nlds, const float o[3], const float d[3], int32_t budget) {
+                                     uint32_t nlds, uint32_t* __restrict__ path, const float o[3], const float d[3], int32_t budget) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -426,7 +452,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     par.valid = false;
     par.mask = 0ull;
@@ -434,20 +460,65 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
+    bool pend = false;  // a brick is held for stepping (postponed until the wave flushes bricks)
+    uint32_t bref = 0u, binfo = 0u;
+    uint64_t bmask = 0ull;
     while (!done) {
-        // the voxel just entered is untested
-        uint32_t w[3];
-        wrap3(R, wm, w);
-        uint32_t sh = 0u, bref = 0u, binfo = 0u;
-        uint64_t bmask = 0ull;
-        const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, w, par, sh, bmask, bref, binfo, st);
-        if (kind == R_SOLID) {
-            hit = true;
-            mat = binfo >> 16;
-            done = true;
-        } else if (kind == R_BRICK) {
-            if (STATS) st.bricks++;
+        if (!pend) {
+            // the voxel just entered is untested
+            if (STATS) st.wv_iters += wave_lead();
+            uint32_t w[3];
+            wrap3(R, wm, w);
+            uint32_t sh = 0u;
+            const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, path, w, par, sh, bmask, bref, binfo, st);
+            if (kind == R_SOLID) {
+                hit = true;
+                mat = binfo >> 16;
+                done = true;
+            } else if (kind == R_BRICK) {
+                if (STATS) st.bricks++;
+                pend = true;
+            } else if (R.steps <= 0) {
+                done = true;
+            } else if (!(fast && [&] {
+                           int32_t ex[3];
+                           box_exits(w, R.s, sh, par.mask, ex);
+                           return skip_box(R, ex);
+                       }())) {
+                if (STATS && fast) st.skip_out++;
+                // step through the cell without lookups (budget ends inside it, or not exact)
+                const uint32_t c[3] = {w[0], w[1], w[2]};
+                bool left = false;
+                while (R.steps > 0) {
+                    dda_step(R);
+                    if (STATS) st.plain_steps++;
+                    wrap3(R, wm, w);
+                    if (!same_cell(w, c, sh)) {
+                        left = true;
+                        break;
+                    }
+                }
+                done = !left;
+            } else if (STATS) {
+                st.skips++;
+                st.wv_skips += wave_lead();
+                st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
+            }
+        }
+#if SVO_PEND8
+        // Postponed brick stepping (speculative leaf postponement, Aila & Laine 2009): lanes that
+        // reached a brick wait while the others keep crossing the tree, and the wave steps the
+        // bricks together once SVO_PEND8/8 of its tracing lanes hold one.
+        const uint64_t waiting = __ballot(pend), tracing = __ballot(!done);
+        const bool flush = (uint32_t)__popcll(waiting) * 8u >= (uint32_t)__popcll(tracing) * (uint32_t)SVO_PEND8;
+#else
+        const bool flush = true;
+#endif
+        if (pend && flush) {
+            pend = false;
             // voxel steps inside the brick, solid mask in registers
+            uint32_t w[3];
+            wrap3(R, wm, w);
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
                 const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
@@ -477,34 +548,13 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 #else
                 dda_step(R);
 #endif
-                if (STATS) st.brick_steps++;
+                if (STATS) {
+                    st.brick_steps++;
+                    st.wv_brick += wave_lead();
+                }
                 wrap3(R, wm, w);
                 if (!same_cell(w, c, 2u)) break;
             }
-        } else if (R.steps <= 0) {
-            done = true;
-        } else if (!(fast && [&] {
-                       int32_t ex[3];
-                       box_exits(w, R.s, sh, par.mask, ex);
-                       return skip_box(R, ex);
-                   }())) {
-            if (STATS && fast) st.skip_out++;
-            // step through the cell without lookups (budget ends inside it, or not exact)
-            const uint32_t c[3] = {w[0], w[1], w[2]};
-            bool left = false;
-            while (R.steps > 0) {
-                dda_step(R);
-                if (STATS) st.plain_steps++;
-                wrap3(R, wm, w);
-                if (!same_cell(w, c, sh)) {
-                    left = true;
-                    break;
-                }
-            }
-            done = !left;
-        } else if (STATS) {
-            st.skips++;
-            st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
         }
     }
     if (STATS) {
@@ -524,6 +574,13 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         atomicAdd(P.stats + 6, (unsigned long long)st.plain_steps);
         for (int k = 0; k < 4; k++) atomicAdd(P.stats + 9 + k, (unsigned long long)st.skip_by_sh[k]);
         atomicAdd(P.stats + 13, (unsigned long long)st.bricks);
+        atomicAdd(P.stats + 14, (unsigned long long)st.wv_iters);
+        atomicAdd(P.stats + 15, (unsigned long long)st.wv_brick);
+        atomicAdd(P.stats + 16, (unsigned long long)st.lds_reads);
+        atomicAdd(P.stats + 17, (unsigned long long)st.root_starts);
+        atomicAdd(P.stats + 18, (unsigned long long)st.cache_empty);
+        atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
+        atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
     }
     Hit h;
     h.x = R.r[0];
@@ -553,6 +610,9 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     __shared__ Node lds[kLdsNodes];
     const uint32_t nlds = P.lds_nodes;
     for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
+    // per-lane node path (node index at each interior depth of the last descent), [depth][lane]
+    __shared__ uint32_t path_lds[(kMaxLevels - 1) * kBlock];
+    uint32_t* const path = path_lds + threadIdx.x;
     // hemisphere AO sample set, broadcast from LDS
     __shared__ float ao_tab[3 * 64];
     if (AO)
@@ -611,7 +671,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, lds, nlds, o, d, P.steps);
+        const Hit h = trace<STATS>(P, rsrc, lds, nlds, path, o, d, P.steps);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -627,7 +687,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                     const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
                     float ad[3];
                     ao_dir(hv, ax, -st, ad);
-                    const Hit a = trace<false>(P, rsrc, lds, nlds, ao_o, ad, P.ao_steps);
+                    const Hit a = trace<false>(P, rsrc, lds, nlds, path, ao_o, ad, P.ao_steps);
                     cnt += (a.info & HIT_BIT) ? 1u : 0u;
                 }
             }
@@ -638,8 +698,8 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-            P.stats[16 + 2 * blockIdx.x] = t_start;
-            P.stats[16 + 2 * blockIdx.x + 1] = t_end;
+            P.stats[SVO_STATS_HEADER + 2 * blockIdx.x] = t_start;
+            P.stats[SVO_STATS_HEADER + 2 * blockIdx.x + 1] = t_end;
         }
     }
 }
