@@ -165,7 +165,8 @@ typedef struct {
                           size (4 slots), brick visits, wave-level loop iterations,
                           wave-level brick voxel steps, LDS node reads, lookups started at
                           the root, lookups answered by the cached parent, wave-level
-                          crossings, wave-level descent levels; then 2 stamps per block
+                          crossings, wave-level descent levels, lookups restarted from the
+                          per-lane path; then 2 stamps per block
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
 

@@ -69,7 +69,10 @@ struct CastParams {
 };
 
 constexpr int kBlock = 256;
-constexpr uint32_t kLdsNodes = 512;  // 8 KB of LDS per block
+#ifndef SVO_LDS_NODES
+#define SVO_LDS_NODES 80
+#endif
+constexpr uint32_t kLdsNodes = SVO_LDS_NODES;  // root + first level (1.25 KB of LDS per block)
 constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
 #ifndef SVO_PEND8
 #define SVO_PEND8 0
@@ -303,7 +306,8 @@ struct Stats {
     uint32_t wv_iters, wv_brick;  // wave-level executions (counted on the first active lane): outer
                                   // loop iterations, brick voxel steps
     uint32_t lds_reads, root_starts, cache_empty;  // LDS node reads; lookups started at the root;
-                                                   // lookups answered by the cached parent mask
+                                                   // lookups answered by the parent mask
+    uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
 };
 
@@ -331,6 +335,12 @@ enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
 // the descent at most one level down; leaving the parent's region restarts at the root, whose top
 // levels are staged in LDS.
+// per-lane path of the last descent in LDS (element [depth * kBlock])
+struct Path {
+    uint64_t* __restrict__ mask;
+    uint32_t* __restrict__ ref;
+};
+
 struct Parent {
     uint64_t mask;
     uint32_t ref;
@@ -352,13 +362,26 @@ __device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uin
 
 template <bool STATS>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                           uint32_t nlds, uint32_t* __restrict__ path, const uint32_t w[3], Parent& par,
+                                           uint32_t nlds, const Path& path, const uint32_t w[3], Parent& par,
                                            uint32_t& sh_out, uint64_t& bmask, uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
     const uint32_t diff = (w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2]);
-    if (par.valid && (diff >> (par.sh + 2u)) == 0u) {
+    if (par.valid) {
+        if ((diff >> (par.sh + 2u)) != 0u) {
+            // left the parent's region: the deepest node of the last descent whose region also
+            // holds this cell (depth levels-1-floor(h/2), h = highest differing bit) becomes the
+            // parent, read back from the per-lane path in LDS
+            const int32_t da = P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1);
+            par.mask = path.mask[da * kBlock];
+            par.ref = path.ref[da * kBlock];
+            par.sh = (uint32_t)(2 * (P.levels - 1 - da));
+            par.w[0] = w[0];
+            par.w[1] = w[1];
+            par.w[2] = w[2];
+            if (STATS) st.path_starts++;
+        }
         const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
         if (!((par.mask >> sl) & 1ull)) {
             sh_out = par.sh;
@@ -367,11 +390,6 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
         }
         ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
-    } else if (par.valid) {
-        // restart at the deepest node of the previous path whose region also holds this cell:
-        // depth levels-1-floor(h/2), h = highest bit in which the two positions differ
-        dd = P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1);
-        ni = path[dd * kBlock];
     } else if (STATS) {
         st.root_starts++;
     }
@@ -394,7 +412,8 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             return kind == K_SOLID ? R_SOLID : R_BRICK;
         }
         const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
-        path[dd * kBlock] = ni;
+        path.mask[dd * kBlock] = n.mask;
+        path.ref[dd * kBlock] = n.ref;
         par.mask = n.mask;
         par.ref = n.ref;
         par.sh = sh;
@@ -430,7 +449,7 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 // One ray with castRayFromCam semantics.
 template <bool STATS>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                     uint32_t nlds, uint32_t* __restrict__ path, const float o[3], const float d[3], int32_t budget) {
+                                     uint32_t nlds, const Path& path, const float o[3], const float d[3], int32_t budget) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -452,7 +471,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     par.valid = false;
     par.mask = 0ull;
@@ -581,6 +600,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         atomicAdd(P.stats + 18, (unsigned long long)st.cache_empty);
         atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
+        atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
     }
     Hit h;
     h.x = R.r[0];
@@ -610,9 +630,11 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     __shared__ Node lds[kLdsNodes];
     const uint32_t nlds = P.lds_nodes;
     for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
-    // per-lane node path (node index at each interior depth of the last descent), [depth][lane]
-    __shared__ uint32_t path_lds[(kMaxLevels - 1) * kBlock];
-    uint32_t* const path = path_lds + threadIdx.x;
+    // per-lane node path (mask and first-child index of the interior node at each depth of the
+    // last descent), [depth][lane]
+    __shared__ uint64_t path_mask[(kMaxLevels - 1) * kBlock];
+    __shared__ uint32_t path_ref[(kMaxLevels - 1) * kBlock];
+    const Path path = {path_mask + threadIdx.x, path_ref + threadIdx.x};
     // hemisphere AO sample set, broadcast from LDS
     __shared__ float ao_tab[3 * 64];
     if (AO)
