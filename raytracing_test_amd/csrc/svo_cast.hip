@@ -77,6 +77,9 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #ifndef SVO_PEND8
 #define SVO_PEND8 0
 #endif
+#ifndef SVO_INV_A
+#define SVO_INV_A 1
+#endif
 #ifndef SVO_FMA
 #define SVO_FMA 1
 #endif
@@ -140,6 +143,12 @@ struct Ray {
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
     float tlast;    // crossing value of the last step, as output (f32)
+#if SVO_INV_A
+    float ia[3];    // f32 estimate of 1/absDelta (crossing counts only estimate with it)
+    __device__ __forceinline__ float inv_a(int k) const { return ia[k]; }
+#else
+    __device__ __forceinline__ float inv_a(int k) const { return __builtin_amdgcn_rcpf((float)a(k)); }
+#endif
 #if SVO_A_F64
     __device__ __forceinline__ double a(int k) const { return ad[k]; }
 #else
@@ -207,7 +216,8 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     const uint32_t z1 = s[2] > 0 ? run_hi(zocc, cz) : cz;
     const uint32_t zm = ((2u << z1) - 1u) & ~((1u << z0) - 1u);
     // planes y over the x run x z run: bit y of yocc = the plane holds a solid slot
-    const uint32_t xrep = xm * 0x1111u;
+    const uint32_t xr2 = xm | (xm << 4);
+    const uint32_t xrep = xr2 | (xr2 << 8);  // xm in every y nibble (shifts: v_mul_lo is quarter rate)
     const uint32_t pl = ((zm & 1u) ? xrep : 0u) | ((zm & 2u) ? xrep << 16 : 0u);
     const uint32_t ph = ((zm & 4u) ? xrep : 0u) | ((zm & 8u) ? xrep << 16 : 0u);
     uint32_t q = (lo & pl) | (hi & ph);
@@ -230,8 +240,8 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 // #{ j >= 0 : T + j*a < W }, exact under exact_axis.  k0 = trunc((W-T)/a) from an f32 estimate (error < 1 for counts below 2^20) is at
 // most 2 below the count; the monotone tests T + k0*a < W and T + (k0+1)*a < W (both values exact
 // on the ray's grid) add the rest.
-__device__ __forceinline__ int32_t count_lt_w(double T, double a, double W) {
-    const float q = (float)(W - T) * __builtin_amdgcn_rcpf((float)a);
+__device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, double W) {
+    const float q = (float)(W - T) * inva;
     const int32_t k0 = (int32_t)fmaxf(q, 0.0f);
     const double X = on_grid(T, k0, a);
     const double X1 = X + a;
@@ -265,7 +275,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const bool strict = bx ? false : (by ? k == 0 : k != 2);
-        n[k] = count_lt_w(R.T[k], R.a(k), strict ? V : Vn);
+        n[k] = count_lt_w(R.T[k], R.a(k), R.inv_a(k), strict ? V : Vn);
         total += n[k];
     }
     if (total > R.steps) return false;
@@ -278,8 +288,8 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     // the two other axes: p = (x exits ? y : x), q = (z exits ? y : z)
     const double Tp = bx ? R.T[1] : R.T[0], ap = bx ? R.a(1) : R.a(0);
     const double Tq = bz ? R.T[1] : R.T[2], aq = bz ? R.a(1) : R.a(2);
-    const int32_t cp = count_lt_w(Tp, ap, bx ? Vn : V);  // p is x (strict) unless x exits
-    const int32_t cq = count_lt_w(Tq, aq, bz ? V : Vn);  // q is z (non-strict) unless z exits
+    const int32_t cp = count_lt_w(Tp, ap, __builtin_amdgcn_rcpf((float)ap), bx ? Vn : V);  // p is x (strict) unless x exits
+    const int32_t cq = count_lt_w(Tq, aq, __builtin_amdgcn_rcpf((float)aq), bz ? V : Vn);  // q is z (non-strict) unless z exits
     const int32_t eb = bx ? e[0] : (by ? e[1] : e[2]);
     const int32_t total = eb + cp + cq;
     if (total > R.steps) return false;
@@ -462,6 +472,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
 #endif
         R.s[k] = ax.step;
+#if SVO_INV_A
+        R.ia[k] = __builtin_amdgcn_rcpf((float)ax.adelta);
+#endif
     }
     R.steps = budget;
     R.axis = 3u;
