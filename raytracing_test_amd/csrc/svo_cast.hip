@@ -74,9 +74,6 @@ constexpr int kBlock = 256;
 #endif
 constexpr uint32_t kLdsNodes = SVO_LDS_NODES;  // root + first level (1.25 KB of LDS per block)
 constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
-#ifndef SVO_PEND8
-#define SVO_PEND8 0
-#endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
@@ -492,63 +489,53 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
-    bool pend = false;  // a brick is held for stepping (postponed until the wave flushes bricks)
+    bool pend = false;  // the lookup found a brick: step through it below
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
     while (!done) {
-        if (!pend) {
-            // the voxel just entered is untested
-            if (STATS) st.wv_iters += wave_lead();
-            uint32_t w[3];
-            wrap3(R, wm, w);
-            uint32_t sh = 0u;
-            const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, path, w, par, sh, bmask, bref, binfo, st);
-            if (kind == R_SOLID) {
-                hit = true;
-                mat = binfo >> 16;
-                done = true;
-            } else if (kind == R_BRICK) {
-                if (STATS) st.bricks++;
-                pend = true;
-            } else if (R.steps <= 0) {
-                done = true;
-            } else if (!(fast && [&] {
-                           int32_t ex[3];
-                           box_exits(w, R.s, sh, par.mask, ex);
-                           return skip_box(R, ex);
-                       }())) {
-                if (STATS && fast) st.skip_out++;
-                // step through the cell without lookups (budget ends inside it, or not exact)
-                const uint32_t c[3] = {w[0], w[1], w[2]};
-                bool left = false;
-                while (R.steps > 0) {
-                    dda_step(R);
-                    if (STATS) st.plain_steps++;
-                    wrap3(R, wm, w);
-                    if (!same_cell(w, c, sh)) {
-                        left = true;
-                        break;
-                    }
+        // the voxel just entered is untested
+        if (STATS) st.wv_iters += wave_lead();
+        uint32_t w[3];
+        wrap3(R, wm, w);
+        uint32_t sh = 0u;
+        const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, path, w, par, sh, bmask, bref, binfo, st);
+        if (kind == R_SOLID) {
+            hit = true;
+            mat = binfo >> 16;
+            done = true;
+        } else if (kind == R_BRICK) {
+            if (STATS) st.bricks++;
+            pend = true;
+        } else if (R.steps <= 0) {
+            done = true;
+        } else if (!(fast && [&] {
+                       int32_t ex[3];
+                       box_exits(w, R.s, sh, par.mask, ex);
+                       return skip_box(R, ex);
+                   }())) {
+            if (STATS && fast) st.skip_out++;
+            // step through the cell without lookups (budget ends inside it, or not exact)
+            const uint32_t c[3] = {w[0], w[1], w[2]};
+            bool left = false;
+            while (R.steps > 0) {
+                dda_step(R);
+                if (STATS) st.plain_steps++;
+                wrap3(R, wm, w);
+                if (!same_cell(w, c, sh)) {
+                    left = true;
+                    break;
                 }
-                done = !left;
-            } else if (STATS) {
-                st.skips++;
-                st.wv_skips += wave_lead();
-                st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
             }
+            done = !left;
+        } else if (STATS) {
+            st.skips++;
+            st.wv_skips += wave_lead();
+            st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
         }
-#if SVO_PEND8
-        // Postponed brick stepping (speculative leaf postponement, Aila & Laine 2009): lanes that
-        // reached a brick wait while the others keep crossing the tree, and the wave steps the
-        // bricks together once SVO_PEND8/8 of its tracing lanes hold one.
-        const uint64_t waiting = __ballot(pend), tracing = __ballot(!done);
-        const bool flush = (uint32_t)__popcll(waiting) * 8u >= (uint32_t)__popcll(tracing) * (uint32_t)SVO_PEND8;
-#else
-        const bool flush = true;
-#endif
-        if (pend && flush) {
+        if (pend) {
+            // voxel steps inside the brick, solid mask in registers.  (Postponing bricks until
+            // more lanes hold one, or bounding the steps per iteration, measured slower.)
             pend = false;
-            // voxel steps inside the brick, solid mask in registers
             uint32_t w[3];
             wrap3(R, wm, w);
             const uint32_t c[3] = {w[0], w[1], w[2]};
