@@ -74,17 +74,14 @@ constexpr int kBlock = 256;
 #endif
 constexpr uint32_t kLdsNodes = SVO_LDS_NODES;  // root + first level (1.25 KB of LDS per block)
 constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
+#ifndef SVO_BRICK_FAST
+#define SVO_BRICK_FAST 1
+#endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
 #ifndef SVO_FMA
 #define SVO_FMA 1
-#endif
-#ifndef SVO_SKIP3
-#define SVO_SKIP3 1
-#endif
-#ifndef SVO_BRICK_BOX
-#define SVO_BRICK_BOX 0  // box crossing inside bricks too (A/B)
 #endif
 #ifndef SVO_A_F64
 #define SVO_A_F64 0  // keep absDelta in f64 registers (A/B)
@@ -178,19 +175,17 @@ __device__ __forceinline__ void dda_step(Ray& R) {
     R.steps--;
 }
 
-// steps along one axis until the wrapped coordinate w leaves its aligned 2^sh cell
-__device__ __forceinline__ int32_t exit_steps(uint32_t w, int32_t s, uint32_t sh) {
-    const uint32_t lo = w & ~((1u << sh) - 1u);
-    return s > 0 ? (int32_t)(lo + (1u << sh) - w) : (int32_t)(w - lo + 1u);
+// Free slots of a 4-slot line (bit = occupied) beyond slot c in the step direction, before an
+// occupied slot or the end of the line.  Branch-free.
+__device__ __forceinline__ uint32_t run_fwd(uint32_t occ, uint32_t c, bool pos) {
+    const uint32_t up = (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
+    const uint32_t down = c - (32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u))));
+    return pos ? up : down;
 }
 
-// Run of free slots (4-slot line, bit = occupied) from slot c in the step direction: the last free
-// slot above c (s > 0) or below c (s < 0).  Branch-free.
-__device__ __forceinline__ uint32_t run_hi(uint32_t occ, uint32_t c) {
-    return c + (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
-}
-__device__ __forceinline__ uint32_t run_lo(uint32_t occ, uint32_t c) {
-    return 32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u)));  // one above the nearest occupied slot below
+// slots c .. c+n (pos) or c-n .. c of a 4-slot line
+__device__ __forceinline__ uint32_t run_bits(uint32_t c, uint32_t n, bool pos) {
+    return ((2u << n) - 1u) << (pos ? c : c - n);
 }
 
 // Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
@@ -198,20 +193,19 @@ __device__ __forceinline__ uint32_t run_lo(uint32_t occ, uint32_t c) {
 // the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
 __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, int32_t e[3]) {
     const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
+    const bool px = s[0] > 0, py = s[1] > 0, pz = s[2] > 0;
     const uint32_t lo = (uint32_t)pmask, hi = (uint32_t)(pmask >> 32);
     // x run through the row (cy, cz)
     const uint32_t row = (uint32_t)(pmask >> (16u * cz + 4u * cy)) & 0xFu;
-    const uint32_t x0 = s[0] > 0 ? cx : run_lo(row, cx);
-    const uint32_t x1 = s[0] > 0 ? run_hi(row, cx) : cx;
-    const uint32_t xm = ((2u << x1) - 1u) & ~((1u << x0) - 1u);
+    const uint32_t nx = run_fwd(row, cx, px);
+    const uint32_t xm = run_bits(cx, nx, px);
     // rows (cy, z) over the x run: bit z of zocc = the row holds a solid slot
     const uint32_t xm2 = (xm | (xm << 16)) << (4u * cy);
     const uint32_t tl = lo & xm2, th = hi & xm2;
     const uint32_t zocc = (uint32_t)((tl & 0xFFFFu) != 0u) | ((uint32_t)(tl > 0xFFFFu) << 1) |
                           ((uint32_t)((th & 0xFFFFu) != 0u) << 2) | ((uint32_t)(th > 0xFFFFu) << 3);
-    const uint32_t z0 = s[2] > 0 ? cz : run_lo(zocc, cz);
-    const uint32_t z1 = s[2] > 0 ? run_hi(zocc, cz) : cz;
-    const uint32_t zm = ((2u << z1) - 1u) & ~((1u << z0) - 1u);
+    const uint32_t nz = run_fwd(zocc, cz, pz);
+    const uint32_t zm = run_bits(cz, nz, pz);
     // planes y over the x run x z run: bit y of yocc = the plane holds a solid slot
     const uint32_t xr2 = xm | (xm << 4);
     const uint32_t xrep = xr2 | (xr2 << 8);  // xm in every y nibble (shifts: v_mul_lo is quarter rate)
@@ -222,14 +216,12 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     q |= q >> 1;
     q |= q >> 2;
     const uint32_t yocc = (q & 1u) | ((q >> 3) & 2u) | ((q >> 6) & 4u) | ((q >> 9) & 8u);
-    const uint32_t y0 = s[1] > 0 ? cy : run_lo(yocc, cy);
-    const uint32_t y1 = s[1] > 0 ? run_hi(yocc, cy) : cy;
-    const uint32_t lo3[3] = {x0, y0, z0}, hi3[3] = {x1, y1, z1};
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const uint32_t base = (w[k] >> (sh + 2u)) << (sh + 2u);
-        e[k] = s[k] > 0 ? (int32_t)(base + ((hi3[k] + 1u) << sh) - w[k]) : (int32_t)(w[k] - (base + (lo3[k] << sh)) + 1u);
-    }
+    const uint32_t ny = run_fwd(yocc, cy, py);
+    // steps to leave: the n further cells, plus the steps to leave the current cell
+    const uint32_t m = (1u << sh) - 1u;
+    e[0] = (int32_t)((nx << sh) + ((px ? ~w[0] : w[0]) & m) + 1u);
+    e[1] = (int32_t)((ny << sh) + ((py ? ~w[1] : w[1]) & m) + 1u);
+    e[2] = (int32_t)((nz << sh) + ((pz ? ~w[2] : w[2]) & m) + 1u);
 }
 
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
@@ -259,14 +251,12 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
     const bool by = !bx && (E[1] < E[2]);
-    const bool bz = !bx && !by;
     const double V = bx ? E[0] : (by ? E[1] : E[2]);
     // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
     // (rank_k > rank_b, i.e. k < b), else T + j*a <= V, which on doubles is < nextup(V).
     const uint64_t vb = (uint64_t)__double_as_longlong(V);
     const double Vn = V > 0.0 ? __longlong_as_double((long long)(vb + 1u))
                               : (V < 0.0 ? __longlong_as_double((long long)(vb - 1u)) : __longlong_as_double(1ll));
-#if SVO_SKIP3
     // every axis through the same count: the exit axis b counts to exactly e_b against nextup(V)
     int32_t total = 0, n[3];
 #pragma unroll
@@ -279,27 +269,8 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
-        R.r[k] += R.s[k] * n[k];
+        R.r[k] += R.s[k] > 0 ? n[k] : -n[k];  // s = +-1 (no integer multiply)
     }
-#else
-    // the two other axes: p = (x exits ? y : x), q = (z exits ? y : z)
-    const double Tp = bx ? R.T[1] : R.T[0], ap = bx ? R.a(1) : R.a(0);
-    const double Tq = bz ? R.T[1] : R.T[2], aq = bz ? R.a(1) : R.a(2);
-    const int32_t cp = count_lt_w(Tp, ap, __builtin_amdgcn_rcpf((float)ap), bx ? Vn : V);  // p is x (strict) unless x exits
-    const int32_t cq = count_lt_w(Tq, aq, __builtin_amdgcn_rcpf((float)aq), bz ? V : Vn);  // q is z (non-strict) unless z exits
-    const int32_t eb = bx ? e[0] : (by ? e[1] : e[2]);
-    const int32_t total = eb + cp + cq;
-    if (total > R.steps) return false;
-    const int32_t n0 = bx ? eb : cp;
-    const int32_t n1 = bx ? cp : (by ? eb : cq);
-    const int32_t n2 = bz ? eb : cq;
-    R.T[0] = on_grid(R.T[0], n0, R.a(0));
-    R.T[1] = on_grid(R.T[1], n1, R.a(1));
-    R.T[2] = on_grid(R.T[2], n2, R.a(2));
-    R.r[0] += R.s[0] * n0;
-    R.r[1] += R.s[1] * n1;
-    R.r[2] += R.s[2] * n2;
-#endif
     R.tlast = (float)V;
     R.axis = bx ? 0u : (by ? 1u : 2u);
     R.steps -= total;
@@ -538,6 +509,54 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             pend = false;
             uint32_t w[3];
             wrap3(R, wm, w);
+#if SVO_BRICK_FAST
+            // Voxel index v and per-axis steps left in the brick (one byte each) are stepped
+            // instead of positions; positions follow from the step counts when the brick ends.
+            uint32_t v = child_slot(w[0], w[1], w[2], 0u);
+            const int32_t dvx = R.s[0], dvy = R.s[1] * 4, dvz = R.s[2] * 16;
+            const uint32_t ex = R.s[0] > 0 ? 4u - (w[0] & 3u) : (w[0] & 3u) + 1u;
+            const uint32_t ey = R.s[1] > 0 ? 4u - (w[1] & 3u) : (w[1] & 3u) + 1u;
+            const uint32_t ez = R.s[2] > 0 ? 4u - (w[2] & 3u) : (w[2] & 3u) + 1u;
+            const uint32_t left0 = ex | (ey << 8) | (ez << 16);
+            uint32_t left = left0;
+            bool solid, go;
+            do {  // one exit: the compiler keeps the state in place (no per-exit copies)
+                solid = (bmask >> v) & 1ull;
+                go = !solid && R.steps > 0;
+                if (go) {
+                    // one DDA step (ray_caster.cpp:70-80) without position updates
+                    const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+                    const bool cy = !cx && (R.T[1] < R.T[2]);
+                    const bool cz = !cx && !cy;
+                    R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+                    R.axis = cx ? 0u : (cy ? 1u : 2u);
+                    R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+                    R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+                    R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
+                    R.steps--;
+                    v += (uint32_t)(cx ? dvx : (cy ? dvy : dvz));
+                    left -= cx ? 1u : (cy ? 0x100u : 0x10000u);
+                    if (STATS) {
+                        st.brick_steps++;
+                        st.wv_brick += wave_lead();
+                    }
+                    go = ((left - 0x010101u) & ~left & 0x808080u) == 0u;  // no byte at 0: still inside
+                }
+            } while (go);
+            if (solid) {
+                hit = true;
+                mat = brick_material(P, bmask, bref, binfo, v);
+                done = true;
+            } else if (R.steps <= 0 && (((left - 0x010101u) & ~left & 0x808080u) == 0u)) {
+                done = true;  // budget ended inside the brick
+            }
+            const int32_t nx = (int32_t)((left0 & 0xFFu) - (left & 0xFFu));
+            const int32_t ny = (int32_t)(((left0 >> 8) & 0xFFu) - ((left >> 8) & 0xFFu));
+            const int32_t nz = (int32_t)((left0 >> 16) - (left >> 16));
+            R.r[0] += R.s[0] > 0 ? nx : -nx;
+            R.r[1] += R.s[1] > 0 ? ny : -ny;
+            R.r[2] += R.s[2] > 0 ? nz : -nz;
+#else
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
                 const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
@@ -551,22 +570,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                     done = true;
                     break;
                 }
-#if SVO_BRICK_BOX
-                if (fast) {
-                    // cross the forward box of empty voxels of this brick in one move
-                    int32_t ex[3];
-                    box_exits(w, R.s, 0u, bmask, ex);
-                    if (!skip_box(R, ex)) {
-                        while (R.steps > 0) dda_step(R);  // the budget ends inside the empty box
-                        done = true;
-                        break;
-                    }
-                } else {
-                    dda_step(R);
-                }
-#else
                 dda_step(R);
-#endif
                 if (STATS) {
                     st.brick_steps++;
                     st.wv_brick += wave_lead();
@@ -574,6 +578,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 wrap3(R, wm, w);
                 if (!same_cell(w, c, 2u)) break;
             }
+#endif
         }
     }
     if (STATS) {
