@@ -163,7 +163,7 @@ typedef struct {
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
                           lane work units, wave-max work units x 64, crossings by box cell
                           size (4 slots), brick visits, wave-level loop iterations,
-                          wave-level brick voxel steps, LDS node reads, lookups started at
+                          wave-level brick voxel steps, (reserved), lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
                           per-lane path; then 2 stamps per block

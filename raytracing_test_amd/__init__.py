@@ -39,7 +39,7 @@ CAST_TIMELINE = 32  # per-block start/end stamps only
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
-              "lds_reads", "root_starts", "cache_empty", "wave_skips", "wave_descents",
+              "reserved16", "root_starts", "cache_empty", "wave_skips", "wave_descents",
               "path_starts")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 

@@ -48,7 +48,6 @@ struct CastParams {
     int32_t steps;
     int32_t flags;
     unsigned long long* stats;
-    uint32_t lds_nodes;
     // frame mode
     RayGen rg;
     float org[3];
@@ -69,10 +68,6 @@ struct CastParams {
 };
 
 constexpr int kBlock = 256;
-#ifndef SVO_LDS_NODES
-#define SVO_LDS_NODES 80
-#endif
-constexpr uint32_t kLdsNodes = SVO_LDS_NODES;  // root + first level (1.25 KB of LDS per block)
 constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
 #ifndef SVO_BRICK_FAST
 #define SVO_BRICK_FAST 1
@@ -283,8 +278,8 @@ struct Stats {
     uint32_t bricks;         // brick visits
     uint32_t wv_iters, wv_brick;  // wave-level executions (counted on the first active lane): outer
                                   // loop iterations, brick voxel steps
-    uint32_t lds_reads, root_starts, cache_empty;  // LDS node reads; lookups started at the root;
-                                                   // lookups answered by the parent mask
+    uint32_t root_starts, cache_empty;  // lookups started at the root; lookups answered by the
+                                        // parent mask
     uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
 };
@@ -339,14 +334,14 @@ __device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uin
 }
 
 template <bool STATS>
-__device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                           uint32_t nlds, const Path& path, const uint32_t w[3], Parent& par,
-                                           uint32_t& sh_out, uint64_t& bmask, uint32_t& bref, uint32_t& binfo, Stats& st) {
+__device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
+                                           const uint32_t w[3], Parent& par, uint32_t& sh_out, uint64_t& bmask,
+                                           uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
-    const uint32_t diff = (w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2]);
     if (par.valid) {
+        const uint32_t diff = (w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2]);
         if ((diff >> (par.sh + 2u)) != 0u) {
             // left the parent's region: the deepest node of the last descent whose region also
             // holds this cell (depth levels-1-floor(h/2), h = highest differing bit) becomes the
@@ -361,8 +356,8 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             if (STATS) st.path_starts++;
         }
         const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
+        sh_out = par.sh;
         if (!((par.mask >> sl) & 1ull)) {
-            sh_out = par.sh;
             if (STATS) st.cache_empty++;
             return R_EMPTY;
         }
@@ -371,43 +366,43 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
     } else if (STATS) {
         st.root_starts++;
     }
-    for (; dd < P.levels; dd++) {
-        Node n;
-        if (STATS) st.wv_descents += wave_lead();
-        if (ni < nlds) {
-            n = lds[ni];
-            if (STATS) st.lds_reads++;
-        } else {
-            n = load_node(rsrc, ni);
-            if (STATS) st.loads++;
+    // descend (one exit: no per-exit register copies)
+    uint32_t res = R_EMPTY;
+    bool more = dd < P.levels;
+    while (more) {
+        if (STATS) {
+            st.wv_descents += wave_lead();
+            st.loads++;
         }
+        const Node n = load_node(rsrc, ni);
         const uint32_t kind = n.info & K_KIND_MASK;
-        if (kind != K_INTERIOR) {
+        if (kind == K_INTERIOR) {
+            const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
+            path.mask[dd * kBlock] = n.mask;
+            path.ref[dd * kBlock] = n.ref;
+            par.mask = n.mask;
+            par.ref = n.ref;
+            par.sh = sh;
+            par.w[0] = w[0];
+            par.w[1] = w[1];
+            par.w[2] = w[2];
+            par.valid = true;
+            const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
+            const bool occ = (n.mask >> sl) & 1ull;
+            ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
+            dd++;
+            more = occ && dd < P.levels;
+            sh_out = occ ? 0u : sh;  // (occupied at the last level only in a malformed tree: one voxel)
+        } else {
             bmask = n.mask;
             bref = n.ref;
             binfo = n.info;
             sh_out = 2u;
-            return kind == K_SOLID ? R_SOLID : R_BRICK;
+            res = kind == K_SOLID ? R_SOLID : R_BRICK;
+            more = false;
         }
-        const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
-        path.mask[dd * kBlock] = n.mask;
-        path.ref[dd * kBlock] = n.ref;
-        par.mask = n.mask;
-        par.ref = n.ref;
-        par.sh = sh;
-        par.w[0] = w[0];
-        par.w[1] = w[1];
-        par.w[2] = w[2];
-        par.valid = true;
-        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
-        if (!((n.mask >> sl) & 1ull)) {
-            sh_out = sh;
-            return R_EMPTY;
-        }
-        ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
     }
-    sh_out = 0u;  // malformed tree: treat as a one-voxel empty cell
-    return R_EMPTY;
+    return res;
 }
 
 __device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t mask, uint32_t ref, uint32_t info, uint32_t v) {
@@ -426,8 +421,8 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 
 // One ray with castRayFromCam semantics.
 template <bool STATS>
-__device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Node* __restrict__ lds,
-                                     uint32_t nlds, const Path& path, const float o[3], const float d[3], int32_t budget) {
+__device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
+                                     const float d[3], int32_t budget) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -452,7 +447,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     par.valid = false;
     par.mask = 0ull;
@@ -469,7 +464,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         uint32_t w[3];
         wrap3(R, wm, w);
         uint32_t sh = 0u;
-        const uint32_t kind = lookup<STATS>(P, rsrc, lds, nlds, path, w, par, sh, bmask, bref, binfo, st);
+        const uint32_t kind = lookup<STATS>(P, rsrc, path, w, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
             hit = true;
             mat = binfo >> 16;
@@ -600,7 +595,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         atomicAdd(P.stats + 13, (unsigned long long)st.bricks);
         atomicAdd(P.stats + 14, (unsigned long long)st.wv_iters);
         atomicAdd(P.stats + 15, (unsigned long long)st.wv_brick);
-        atomicAdd(P.stats + 16, (unsigned long long)st.lds_reads);
         atomicAdd(P.stats + 17, (unsigned long long)st.root_starts);
         atomicAdd(P.stats + 18, (unsigned long long)st.cache_empty);
         atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
@@ -631,10 +625,6 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
     if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
-    // top of the breadth-first array (root + the first levels) staged in LDS
-    __shared__ Node lds[kLdsNodes];
-    const uint32_t nlds = P.lds_nodes;
-    for (uint32_t i = threadIdx.x; i < nlds; i += kBlock) lds[i] = P.nodes[i];
     // per-lane node path (mask and first-child index of the interior node at each depth of the
     // last descent), [depth][lane]
     __shared__ uint64_t path_mask[(kMaxLevels - 1) * kBlock];
@@ -698,7 +688,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, lds, nlds, path, o, d, P.steps);
+        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -714,7 +704,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                     const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
                     float ad[3];
                     ao_dir(hv, ax, -st, ad);
-                    const Hit a = trace<false>(P, rsrc, lds, nlds, path, ao_o, ad, P.ao_steps);
+                    const Hit a = trace<false>(P, rsrc, path, ao_o, ad, P.ao_steps);
                     cnt += (a.info & HIT_BIT) ? 1u : 0u;
                 }
             }
@@ -740,7 +730,6 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.steps = d->steps;
     P.flags = d->flags;
     P.stats = reinterpret_cast<unsigned long long*>(d->stats);
-    P.lds_nodes = t->lds_nodes;
     P.org[0] = d->origin[0];
     P.org[1] = d->origin[1];
     P.org[2] = d->origin[2];
@@ -815,13 +804,6 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
     t->device = device;
     t->device_bytes = nb + mb + wb;
-    // stage whole levels from the top while they fit kLdsNodes
-    uint64_t acc = 0;
-    for (int lv = 0; lv < t->levels && lv < 8; lv++) {
-        if (acc + t->nodes_per_level[lv] > kLdsNodes) break;
-        acc += t->nodes_per_level[lv];
-    }
-    t->lds_nodes = (uint32_t)std::min<uint64_t>(acc, t->nodes.size());
     t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
     t->work_next = 0;
     return SVO_OK;
@@ -884,7 +866,6 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.mode = MODE_SINGLE;
     P.steps = steps;
-    P.lds_nodes = t->lds_nodes;
     for (int a = 0; a < 3; a++) {
         P.org[a] = pos[a];
         P.sdir[a] = dir[a];

@@ -50,7 +50,6 @@ struct svo_tree {
     uint32_t work_slots = 0;
     uint32_t work_next = 0;
     uint64_t device_bytes = 0;
-    uint32_t lds_nodes = 0;   // top-of-tree nodes staged in LDS by the cast kernel
 };
 
 namespace svo {
