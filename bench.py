@@ -207,7 +207,7 @@ def main():
         nblk = (rt.Tree.count(descs[0]) + 255) // 256
         d0 = descs[0]
         for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
-            st = torch.zeros(rt.STATS_HEADER + 2 * nblk, dtype=torch.int64, device=dev)
+            st = torch.zeros(rt.STATS_HEADER + 2 * nblk + W * H, dtype=torch.int64, device=dev)
             d0.flags |= mode
             d0.stats = st.data_ptr()
             tree.cast(d0, outs[0], stream)
@@ -216,11 +216,13 @@ def main():
             allv = st.cpu().numpy()
             if mode == rt.CAST_STATS:
                 vals = allv[:rt.STATS_HEADER]
+                if os.environ.get("SVO_RAY_WORK"):  # per-pixel lookups / brick steps for offline analysis
+                    np.save(os.environ["SVO_RAY_WORK"], allv[rt.STATS_HEADER + 2 * nblk:])
                 per = [v / max(1, vals[0]) * (64 if k.startswith("wave_") and not k.endswith("_x64") else 1) for k, v in zip(rt.STAT_NAMES, vals)]
                 print("stats per ray (wave_* per wave): " + ", ".join("%s=%.3f" % (k, v) for k, v in zip(rt.STAT_NAMES, per)) +
                       "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
                 continue
-            stamps = allv[rt.STATS_HEADER:].reshape(-1, 2).astype(np.float64) / 100.0  # us (s_memrealtime = 100 MHz)
+            stamps = allv[rt.STATS_HEADER:rt.STATS_HEADER + 2 * nblk].reshape(-1, 2).astype(np.float64) / 100.0  # us (100 MHz)
             t0s = stamps[:, 0].min()
             dur = stamps[:, 1] - stamps[:, 0]
             span = stamps[:, 1].max() - t0s

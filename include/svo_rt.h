@@ -166,7 +166,8 @@ typedef struct {
                           wave-level brick voxel steps, (reserved), lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
-                          per-lane path; then 2 stamps per block
+                          per-lane path; then 2 stamps per block; then, with SVO_CAST_STATS
+                          in frame mode, one word per output pixel: lookups | brick steps << 32
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
 

@@ -422,7 +422,7 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 // One ray with castRayFromCam semantics.
 template <bool STATS>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
-                                     const float d[3], int32_t budget) {
+                                     const float d[3], int32_t budget, unsigned long long* ray_work = nullptr) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -600,6 +600,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
+        if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
     }
     Hit h;
     h.x = R.r[0];
@@ -647,14 +648,16 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
     if (P.mode == MODE_FRAME) {
-        // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes
-        const int64_t tile = g >> 6;
-        const int32_t lane = (int32_t)(g & 63);
-        int32_t trl = (int32_t)(tile / P.tiles_x);
+        // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes.
+        // The tile index is wave-uniform: its division runs on the scalar unit.
+        const uint32_t tile = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int32_t lane = (int32_t)(threadIdx.x & 63u);
+        const uint32_t tq = tile / (uint32_t)P.tiles_x;
+        int32_t trl = (int32_t)tq;
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
         if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
-        const int32_t tx = (int32_t)(tile - (int64_t)(tile / P.tiles_x) * P.tiles_x);
+        const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         const int32_t px = tx * 8 + (lane & 7), py = tr * 8 + (lane >> 3);
         if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
@@ -688,7 +691,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps);
+        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x + out : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -757,6 +760,8 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.tile_row_step = d->tile_row_step;
     const int32_t tile_rows = (d->height + 7) / 8;
     P.tile_rows_local = d->tile_row_start < tile_rows ? (tile_rows - d->tile_row_start + d->tile_row_step - 1) / d->tile_row_step : 0;
+    if ((int64_t)P.tile_rows_local * P.tiles_x >= (int64_t)1 << 31)
+        SVO_FAIL(SVO_EINVAL, "svo_cast_rays: frame too large (2^31 tiles of 8x8 pixels or more)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * 64;
     return SVO_OK;
 }
