@@ -36,7 +36,8 @@ extern "C" int svo_version(void) { return SVO_RT_VERSION; }
     } while (0)
 
 static void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t)>& fn) {
-    if (nthreads <= 0) nthreads = (int)std::max(1u, std::thread::hardware_concurrency());
+    // default: the machine's threads, at most 16 (a GPU box exposes many more cores than its share)
+    if (nthreads <= 0) nthreads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     nthreads = (int)std::min<int64_t>(nthreads, std::max<int64_t>(1, n / 64));
     if (nthreads <= 1 || n < 2) {
         fn(0, n);
