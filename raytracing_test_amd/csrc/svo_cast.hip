@@ -101,23 +101,24 @@ struct Hit {
 // (with an exact fix-up).  Rays that fail the test step voxel by voxel (still without memory
 // traffic inside known-empty regions).  Both paths give identical results (tests).
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int dbl_lsb(double x) {
-    const uint64_t b = (uint64_t)__double_as_longlong(x);
-    const int ef = (int)((b >> 52) & 0x7FF);
-    const uint64_t m = b & 0xFFFFFFFFFFFFFull;
-    if (ef == 0) return m ? -1074 + __builtin_ctzll(m) : (1 << 20);
-    return ef - 1075 + __builtin_ctzll(m | (1ull << 52));
-}
-
-__device__ __forceinline__ int dbl_ilogb(double x) {  // x > 0, normal
-    return (int)(((uint64_t)__double_as_longlong(x) >> 52) & 0x7FF) - 1023;
+// lowest set bit (power of two) of |x|: x finite and nonzero; denormals -> 1 << 20 ("not fast")
+__device__ __forceinline__ int dbl_lsb(uint32_t hi, uint32_t lo) {
+    const int e = (int)((hi >> 20) & 0x7FFu);
+    const uint32_t mh = (hi & 0xFFFFFu) | 0x100000u;  // hidden bit
+    const int tz = lo ? (int)__builtin_ctz(lo) : 32 + (int)__builtin_ctz(mh);
+    return e == 0 ? (1 << 20) : e - 1075 + tz;
 }
 
 __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
-    if (!__builtin_isfinite(T) || !__builtin_isfinite(a) || !(a > 0.0)) return false;
-    const int u = min(dbl_lsb(T), dbl_lsb(a));
+    const uint32_t th = (uint32_t)((uint64_t)__double_as_longlong(T) >> 32) & 0x7FFFFFFFu, tl = (uint32_t)__double_as_longlong(T);
+    const uint32_t ah = (uint32_t)((uint64_t)__double_as_longlong(a) >> 32), al = (uint32_t)__double_as_longlong(a);
+    const uint32_t et = th >> 20, ea = (ah >> 20) & 0x7FFu;
+    // a: positive, normal, finite; T: finite (zero allowed: no constraint from it)
+    if ((ah >> 31) || ea == 0u || ea == 0x7FFu || et == 0x7FFu) return false;
+    const int u = (th | tl) ? min(dbl_lsb(th, tl), dbl_lsb(ah, al)) : dbl_lsb(ah, al);
     const double bound = __builtin_fabs(T) + (double)(budget + 2) * a;
-    return dbl_ilogb(bound) + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
+    const int eb = (int)((uint32_t)((uint64_t)__double_as_longlong(bound) >> 52) & 0x7FFu) - 1023;
+    return eb + 1 <= u + 52;  // bound < 2^(u+52): the unrounded bound < 2^(u+53)
 }
 
 struct Ray {
@@ -264,7 +265,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
-        R.r[k] += R.s[k] > 0 ? n[k] : -n[k];  // s = +-1 (no integer multiply)
+        R.r[k] += __mul24(R.s[k], n[k]);  // 24-bit multiply-add: full rate (s = +-1, |n| < 2^21)
     }
     R.tlast = (float)V;
     R.axis = bx ? 0u : (by ? 1u : 2u);
@@ -442,7 +443,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
+    // budget < 2^21 also keeps the f32 count estimates within 1 of the truth (count_lt_w)
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 21) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
                       exact_axis(R.T[2], R.a(2), budget);
     bool hit = false;
     uint32_t mat = 0u;
