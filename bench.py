@@ -204,8 +204,8 @@ def main():
     rays_per_launch = rt.Tree.count(descs[0])
 
     if args.stats and rank == 0:
-        nblk = (rt.Tree.count(descs[0]) + 255) // 256
         d0 = descs[0]
+        nblk = ((W + 7) // 8) * len(range(d0.tile_row_start, (H + 7) // 8, d0.tile_row_step))  # 8x8 tiles: >= blocks
         for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
             st = torch.zeros(rt.STATS_HEADER + 2 * nblk + W * H, dtype=torch.int64, device=dev)
             d0.flags |= mode
@@ -222,7 +222,8 @@ def main():
                 print("stats per ray (wave_* per wave): " + ", ".join("%s=%.3f" % (k, v) for k, v in zip(rt.STAT_NAMES, per)) +
                       "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
                 continue
-            stamps = allv[rt.STATS_HEADER:rt.STATS_HEADER + 2 * nblk].reshape(-1, 2).astype(np.float64) / 100.0  # us (100 MHz)
+            stamps = allv[rt.STATS_HEADER:rt.STATS_HEADER + 2 * nblk].reshape(-1, 2)
+            stamps = stamps[stamps[:, 1] > 0].astype(np.float64) / 100.0  # launched blocks; us (100 MHz)
             t0s = stamps[:, 0].min()
             dur = stamps[:, 1] - stamps[:, 0]
             span = stamps[:, 1].max() - t0s

@@ -166,8 +166,9 @@ typedef struct {
                           wave-level brick voxel steps, (reserved), lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
-                          per-lane path; then 2 stamps per block; then, with SVO_CAST_STATS
-                          in frame mode, one word per output pixel: lookups | brick steps << 32
+                          per-lane path; then 2 stamps per block (room for one block per
+                          8x8 tile); then, with SVO_CAST_STATS in frame mode, one word per
+                          output pixel: lookups | brick steps << 32
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
 
@@ -179,7 +180,8 @@ typedef struct {
 /* svo_cast_desc.flags, scheduling (results identical): frames are dispatched top tile row first
    (longest rays first); this bit restores bottom-first order */
 #define SVO_CAST_BOTTOM_FIRST 4
-/* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[SVO_STATS_HEADER + 2*block] only */
+/* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[SVO_STATS_HEADER + 2*block] only;
+   stats must hold SVO_STATS_HEADER + 2 * (8x8 tiles of the launch) [+ pixels with SVO_CAST_STATS] words */
 #define SVO_STATS_HEADER 32
 #define SVO_CAST_TIMELINE 32
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */

@@ -67,7 +67,10 @@ struct CastParams {
     float ao_tab[3 * 64];
 };
 
-constexpr int kBlock = 256;
+#ifndef SVO_BLOCK
+#define SVO_BLOCK 64
+#endif
+constexpr int kBlock = SVO_BLOCK;  // threads per block: one tile (finer tail at the end of a launch)
 constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
 #ifndef SVO_BRICK_FAST
 #define SVO_BRICK_FAST 1
@@ -693,7 +696,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x + out : nullptr);
+        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
