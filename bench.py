@@ -110,6 +110,9 @@ def main():
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
     ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
+    ap.add_argument("--shade", action="store_true",
+                    help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray), "
+                         "rgba gathered instead of hit records")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
     args = ap.parse_args()
 
@@ -154,6 +157,9 @@ def main():
                                flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao)
         descs.append(d)
         flat, views = shard.alloc_flat(n_pad, torch.device("cuda", dev))
+        if args.shade:  # the image is the product: gather it instead of the hit records
+            views["rgba"] = torch.zeros((n_pad, 4), dtype=torch.float32, device=torch.device("cuda", dev))
+            flat = views["rgba"].view(-1)
         if args.ao:
             views["ao"] = torch.zeros(n_pad, dtype=torch.uint8, device=torch.device("cuda", dev))
         flats.append(flat)
@@ -168,7 +174,10 @@ def main():
             for f in range(nframes):
                 if events is not None:
                     events[f][0].record(stream)
-                tree.cast(descs[f], outs[f], stream)
+                if args.shade:
+                    tree.shade(descs[f], outs[f]["rgba"], out=outs[f], stream=stream)
+                else:
+                    tree.cast(descs[f], outs[f], stream)
                 if events is not None:
                     events[f][1].record(stream)
             if world > 1 and not args.no_gather:
@@ -248,11 +257,14 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                 "bytes_per_ray": round(b_ray, 2), "avg_launch_ms": round(avg_kernel_s * 1e3, 4)}
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and not args.ao:
+    if args.shade:
+        roof = None  # the roofline model (§8d) prices primary traversal only
+    if world == 1 and not args.no_cpu_baseline and not args.ao and not args.shade:
         hits = rt.decode_hits(outs[0])
         cpu = cpu_baseline(ppx, ppy, hits)
     line = {
-        "metric": "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline",
+        "metric": ("shaded primary rays/sec (reflections + sun shadow ray)" if args.shade else
+                   "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
         "value": round(value, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -264,7 +276,9 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols),
-        "config": {"ao_samples": args.ao, "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") +
+        "config": {"ao_samples": args.ao, "shade": args.shade,
+                   "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") +
+                   ("shaded (low_res.frag colour model, 75-step shadow rays): " if args.shade else "") +
                    ("C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080" % args.cols if args.config == "c3" else
                     "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols) +
                    " primary rays per GPU per step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % STEPS,

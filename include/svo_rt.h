@@ -196,6 +196,31 @@ int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir
                           svo_block* block);
 int svo_sync(void* hip_stream);
 
+/* ---------------------------------------------------------------------------- shading ------- */
+/* Shading pass: low_res.frag's colour model over castRayFromCam hits, one float4
+   (r, g, b, 0) per ray in the order of the hit records:
+     miss            -> genSkyBox (low_res.frag:157-168) of the final direction x finalColorMod
+     hit             -> colour x calcLightIntensity (:242-252) x finalColorMod; unless reflected, 0.3 x
+                        colour x finalColorMod when the face turns away from the sun or a shadow ray
+                        (castRayFromCam semantics from the centre of lastPos towards sun_dir,
+                        shadow_steps steps, liquid passes) hits (:361-391)
+     look_at voxel   -> colour x 2 + 0.3 (:340-343)
+   A block with flags & 7 == 3 reflects the ray while budget remains (:170-189, :319-331):
+   the last crossing on the hit axis is undone, that axis's step and direction flip, the DDA
+   continues; finalColorMod *= 0.94 per reflection.  Refraction (flags & 7 == 5) is not modelled:
+   liquid passes (castRayFromCam), refractive solids shade as opaque.  Single precision in the
+   shader's operation order. */
+typedef struct {
+    float sun_dir[3];      /* normalised sunDir (globals.cpp:23: normalize(2,1,4)) */
+    int32_t look_at[3];    /* lookingAtBlock (main.cpp:81,89) */
+    int32_t look_at_valid; /* 0: no highlight */
+    int32_t shadow_steps;  /* 75 (low_res.frag:382) */
+} svo_shade_desc;
+
+/* asynchronous on hip_stream; rgba: device float4 per ray; hits: optional hit records (may be NULL) */
+int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const svo_shade_desc* s, float* rgba, const svo_hits* hits,
+                   void* hip_stream);
+
 /* host helpers shared bit-for-bit with the device code */
 int svo_proj_plane(int32_t width, int32_t height, float* ppx, float* ppy);
 int svo_normalize(const float v[3], float out[3]);

@@ -17,6 +17,7 @@
  *   - buildRay + castRayFromCam (FP64 voxel DDA)         src/ray_caster.cpp:19-87
  *   - per-pixel primary ray generation                   src/shaders/low_res.frag:264-288, src/main.cpp:94
  *   - common-ancestor restart traffic model (E_child)    src/shaders/low_res.frag:493-531
+ *   - shading over castRayFromCam hits (svo_shade_rays)  src/shaders/low_res.frag:139-252,319-391
  *
  * Parity pinning: the reference's GL/GLM/Win32-dependent translation units are unbuildable in this
  * image (no GLM, GLEW, GLFW or windows.h; stand-in headers are not allowed).  Only
@@ -1196,6 +1197,192 @@ EXPORT void orc_cast_frame_ao(const otree* t, const float org[3], const float ca
         j->tid = i; j->nthreads = nthreads;
         j->ao = ao; j->hit = hit;
         pthread_create(&th[i], NULL, o_ao_worker, j);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(jobs);
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Shading, restating include/svo_rt.h's svo_shade_rays contract: low_res.frag's
+ * colour model (genSkyBox :157-168, calcLightIntensity :242-252, shadow ray :373-391, highlight
+ * :340-343, reflectRay :170-189) over castRayFromCam hits.  Single precision, shader op order.
+ * ---------------------------------------------------------------------------------------------- */
+/* o_cast with reflections: a hit on a block with (flags & 7) == 3 while steps remain undoes the
+   last crossing on the hit axis, flips that axis's step and direction, and continues. */
+static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3], const float dir_in[3], int steps, orayres* R,
+                        float dir[3], int* nrefl) {
+    int st[3];
+    double dl[3], ad[3], ex[3], dp[3];
+    int r[3], last[3];
+    for (int a = 0; a < 3; a++) {
+        dir[a] = dir_in[a];
+        st[a] = dir[a] < 0 ? -1 : 1;
+        dl[a] = (double)(1.0f / dir[a]);
+        ad[a] = o_gabs(dl[a]);
+        r[a] = (int)truncf(org[a]);
+        ex[a] = (double)org[a];
+        if (st[a] < 0) ex[a] -= 1;
+    }
+    for (int a = 0; a < 3; a++) dp[a] = ad[a] - (ex[a] - (double)r[a]) * dl[a];
+    memset(R, 0, sizeof(*R));
+    R->axis = -1;
+    *nrefl = 0;
+    for (int a = 0; a < 3; a++) last[a] = r[a];
+    while (steps--) {
+        int ax;
+        for (int a = 0; a < 3; a++) last[a] = r[a];
+        if (dp[0] < dp[1] && dp[0] < dp[2]) ax = 0;
+        else if (dp[1] < dp[2]) ax = 1;
+        else ax = 2;
+        r[ax] += st[ax];
+        R->t = dp[ax];
+        dp[ax] += ad[ax];
+        R->axis = ax;
+        uint32_t f;
+        uint64_t c;
+        float m;
+        if (gb(world, r[0], r[1], r[2], &f, &c, &m)) {
+            R->err = 1;
+            break;
+        }
+        if (c != ~0ull && (f & 0x10) == 0) {
+            if ((f & 7u) == 3u && steps > 0) {
+                dp[ax] -= ad[ax];
+                st[ax] = -st[ax];
+                dir[ax] = -dir[ax];
+                (*nrefl)++;
+                continue;
+            }
+            memcpy(R->pos, r, sizeof(r));
+            memcpy(R->last, last, sizeof(last));
+            R->steps = steps;
+            R->hit = 1;
+            R->flags = f;
+            R->color = c;
+            R->meta = m;
+            return;
+        }
+    }
+    memcpy(R->pos, r, sizeof(r));
+    memcpy(R->last, last, sizeof(last));
+    R->steps = 0;
+    R->hit = 0;
+    R->flags = 0;
+    R->color = ~0ull;
+    R->meta = 0.0f;
+}
+
+static void o_color(uint64_t c, float o[3]) {
+    const double sc = 1.0 / 2097152.0;
+    o[0] = (float)((double)(c >> 42) * sc);
+    o[1] = (float)((double)((c >> 21) & 0x1FFFFFull) * sc);
+    o[2] = (float)((double)(c & 0x1FFFFFull) * sc);
+}
+
+static float o_sigmoid(float x, float scale, float k) { return 1.0f / (1.0f + expf(-x * k)) * scale; }
+static float o_clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+static void o_sky(const float d[3], const float sun[3], float o[3]) {
+    float dy = d[1];
+    if (dy < 0.0f) dy *= 1.4f;
+    float haze = (0.1f - fabsf(o_clampf(dy, -0.3f, 0.3f))) * 0.8f + 0.1f;
+    float modifier = o_clampf(o_sigmoid(1.0f - (haze * 2.0f), 1.0f, 2.0f), 0.0f, 1.0f);
+    float ex = d[0] - sun[0], ey = dy - sun[1], ez = d[2] - sun[2];
+    float b = sqrtf((ex * ex + ey * ey) + ez * ez) * 50.0f;
+    float sv = o_sigmoid(1.5f - b, 1.0f, 1.6f);
+    float h3 = o_clampf(haze, 0.0f, 1.0f) * 3.0f;
+    o[0] = (0.2f + h3) * modifier + sv;
+    o[1] = (0.4f + h3) * modifier + sv;
+    o[2] = (1.0f + h3) * modifier + 0.0f;
+}
+
+static void o_shade(o_getblock_fn gb, const void* world, const float org[3], const float d0[3], int steps, const float sun[3],
+                    const int32_t* look, int shadow_steps, float out[4]) {
+    orayres R;
+    float dir[3];
+    int nrefl;
+    o_cast_refl(gb, world, org, d0, steps, &R, dir, &nrefl);
+    float m = 1.0f;
+    for (int i = 0; i < nrefl; i++) m *= 0.94f;
+    float c[3];
+    if (look && R.pos[0] == look[0] && R.pos[1] == look[1] && R.pos[2] == look[2]) {
+        float b[3];
+        o_color(R.color, b);
+        for (int k = 0; k < 3; k++) c[k] = b[k] * 2.0f + 0.3f;
+    } else if (!R.hit) {
+        float sk[3];
+        o_sky(dir, sun, sk);
+        for (int k = 0; k < 3; k++) c[k] = sk[k] * m;
+    } else {
+        float col[3];
+        o_color(R.color, col);
+        int ax = R.axis;
+        int sg = R.pos[ax] - R.last[ax];
+        float l = sun[ax] * (float)(-sg);
+        int facing = l > 0.0f;
+        float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
+        for (int k = 0; k < 3; k++) c[k] = col[k] * inten * m;
+        int dark = 0;
+        if (nrefl == 0) {
+            if (!facing) {
+                dark = 1;
+            } else {
+                float so[3] = {(float)R.last[0] + 0.5f, (float)R.last[1] + 0.5f, (float)R.last[2] + 0.5f};
+                orayres S;
+                o_cast(gb, world, so, sun, shadow_steps, &S);
+                dark = S.hit != 0;
+            }
+        }
+        if (dark)
+            for (int k = 0; k < 3; k++) c[k] = col[k] * 0.3f * m;
+    }
+    out[0] = c[0];
+    out[1] = c[1];
+    out[2] = c[2];
+    out[3] = 0.0f;
+}
+
+typedef struct {
+    const otree* t;
+    float org[3], cam[3], ppx, ppy, rw, rh, sun[3];
+    int W, H, steps, shadow_steps, tid, nthreads;
+    const int32_t* look;
+    const int64_t* pix;
+    int64_t n;
+    float* rgba;
+} o_shjob;
+static void* o_shade_worker(void* p) {
+    o_shjob* j = (o_shjob*)p;
+    for (int64_t k = j->tid; k < j->n; k += j->nthreads) {
+        int64_t pi = j->pix ? j->pix[k] : k;
+        float d[3];
+        o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
+        o_shade(o_gb_tree, j->t, j->org, d, j->steps, j->sun, j->look, j->shadow_steps, j->rgba + 4 * k);
+    }
+    return NULL;
+}
+EXPORT void orc_shade_frame(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
+                            const float sun[3], const int32_t* look, int shadow_steps, const int64_t* pix, int64_t n, int nthreads,
+                            float* rgba) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    o_shjob* jobs = (o_shjob*)calloc((size_t)nthreads, sizeof(o_shjob));
+    for (int i = 0; i < nthreads; i++) {
+        o_shjob* j = &jobs[i];
+        j->t = t;
+        memcpy(j->org, org, 12);
+        memcpy(j->cam, cam, 12);
+        memcpy(j->sun, sun, 12);
+        j->ppx = ppx; j->ppy = ppy;
+        j->rw = 1.0f / (float)W; j->rh = 1.0f / (float)H;
+        j->W = W; j->H = H; j->steps = steps; j->shadow_steps = shadow_steps;
+        j->look = look;
+        j->pix = pix;
+        j->n = pix ? n : (int64_t)W * H;
+        j->tid = i; j->nthreads = nthreads;
+        j->rgba = rgba;
+        pthread_create(&th[i], NULL, o_shade_worker, j);
     }
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
     free(jobs);

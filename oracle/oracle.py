@@ -122,6 +122,8 @@ def lib(native=False):
     L.orc_hemisphere.argtypes = [C.c_int, _f32p]
     L.orc_cast_frame_ao.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.c_int, vp, vp]
+    L.orc_shade_frame.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, _f32p, vp, C.c_int, vp, C.c_int64,
+                                  C.c_int, vp]
     _libs[path] = L
     return L
 
@@ -276,6 +278,18 @@ class Tree:
         self.L.orc_cast_frame_ao(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, n_ao, ao_steps, _ptr(pix), n, nthreads, _ptr(ao),
                                  _ptr(hit))
         return ao, hit
+
+    def shade_frame(self, org, cam, W, H, steps, sun, look_at=None, shadow_steps=75, ppx=None, ppy=None, pixels=None, nthreads=8):
+        """shaded frame (svo_shade_rays contract, oracle.c §shading): (n, 4) float32 rgba in pixel order"""
+        if ppx is None:
+            ppx, ppy = proj_plane(W, H)
+        n = W * H if pixels is None else len(pixels)
+        pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
+        look = None if look_at is None else np.ascontiguousarray(look_at, dtype=np.int32)
+        rgba = np.zeros((n, 4), np.float32)
+        self.L.orc_shade_frame(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, f3(sun), _ptr(look), shadow_steps, _ptr(pix), n, nthreads,
+                               _ptr(rgba))
+        return rgba
 
     def frame_entries(self, org, cam, W, H, steps, ppx=None, ppy=None, pixels=None, nthreads=8):
         if ppx is None:

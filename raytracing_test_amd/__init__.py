@@ -104,6 +104,14 @@ class Hits(C.Structure):
     _fields_ = [("pos_steps", C.c_void_p), ("t", C.c_void_p), ("info", C.c_void_p), ("ao", C.c_void_p)]
 
 
+class ShadeDesc(C.Structure):
+    _fields_ = [("sun_dir", C.c_float * 3), ("look_at", C.c_int32 * 3), ("look_at_valid", C.c_int32), ("shadow_steps", C.c_int32)]
+
+
+# globals.cpp:23: sun = normalize(vec3(2, 1, 4))
+SUN_DIR = None  # filled lazily by sun_dir() (svo_normalize, bit-identical to the device)
+
+
 _lib = None
 
 # every symbol include/svo_rt.h declares (tests check the library exports all of them)
@@ -114,7 +122,7 @@ ABI_SYMBOLS = (
     "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
-    "svo_build_heightfield",
+    "svo_build_heightfield", "svo_shade_rays",
 )
 
 
@@ -156,6 +164,7 @@ def lib():
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
     L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
+    L.svo_shade_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(ShadeDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_ray_from_cam.argtypes = [vp, f3, f3, i32, C.POINTER(RayResult), C.POINTER(Block)]
     L.svo_sync.argtypes = [vp]
     L.svo_proj_plane.argtypes = [i32, i32, C.POINTER(f32), C.POINTER(f32)]
@@ -464,12 +473,49 @@ class Tree:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return out
 
+    def shade(self, desc, rgba, sun=None, look_at=None, shadow_steps=75, out=None, stream=None):
+        """Launch the shading pass (svo_shade_rays) for `desc`: rgba is a (n, 4) float32 device tensor."""
+        sd = ShadeDesc()
+        sd.sun_dir[:] = [float(x) for x in (sun if sun is not None else sun_dir())]
+        if look_at is not None:
+            sd.look_at[:] = [int(x) for x in look_at]
+            sd.look_at_valid = 1
+        sd.shadow_steps = shadow_steps
+        h = None
+        if out is not None:
+            h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), None)
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_shade_rays(self._h, C.byref(desc), C.byref(sd), C.c_void_p(rgba.data_ptr()), C.byref(h) if h else None,
+                                    C.c_void_p(s) if s else None), "svo_shade_rays")
+
+    def shade_frame(self, origin, cam_dir, width, height, steps=300, sun=None, look_at=None, shadow_steps=75, ppx=None, ppy=None,
+                    tile_row_start=0, tile_row_step=1, with_hits=False, stream=None, sync=True, flags=0):
+        """One shaded frame: (n, 4) float32 rgba in hit-record order (and the hit records with with_hits)."""
+        torch = _torch()
+        d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step, flags, 0, 5)
+        n = self.count(d)
+        dev = self.info().device
+        rgba = torch.empty((n, 4), dtype=torch.float32, device=torch.device("cuda", dev))
+        out = self.alloc_hits(n, dev) if with_hits else None
+        self.shade(d, rgba, sun, look_at, shadow_steps, out, stream)
+        if sync:
+            _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
+        return (rgba, out) if with_hits else rgba
+
     def cast_ray_from_cam(self, pos, cam_dir, steps):
         """RAY_CASTER::castRayFromCam(steps) with the camera passed in: (RayResult, Block)."""
         r, b = RayResult(), Block()
         _check(lib().svo_cast_ray_from_cam(self._h, _f3(pos), _f3(cam_dir), steps, C.byref(r), C.byref(b)),
                "svo_cast_ray_from_cam")
         return (tuple(r.pos), tuple(r.last_pos), r.steps), b.astuple()
+
+
+def sun_dir():
+    """The reference's sun direction, normalize(2, 1, 4) (globals.cpp:23), as the library computes it."""
+    global SUN_DIR
+    if SUN_DIR is None:
+        SUN_DIR = tuple(normalize((2.0, 1.0, 4.0)))
+    return SUN_DIR
 
 
 def decode_hits(out):

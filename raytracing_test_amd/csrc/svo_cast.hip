@@ -65,6 +65,13 @@ struct CastParams {
     // hemisphere AO (A8)
     int32_t ao_n, ao_steps;
     float ao_tab[3 * 64];
+    // shading: palette colours / flags, sun, highlighted block, shadow budget
+    const uint64_t* mat_color;
+    const uint32_t* mat_flags;
+    float4* rgba;
+    float sun[3];
+    int32_t look[3];
+    int32_t look_valid, shadow_steps;
 };
 
 #ifndef SVO_BLOCK
@@ -424,9 +431,16 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 }
 
 // One ray with castRayFromCam semantics.
-template <bool STATS>
+// Reflections of the shading pass (reflectRay, low_res.frag:170-189): direction after them and count.
+struct Bounce {
+    float d[3];
+    int32_t n;
+};
+
+template <bool STATS, bool REFLECT = false>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
-                                     const float d[3], int32_t budget, unsigned long long* ray_work = nullptr) {
+                                     const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
+                                     Bounce* bounce = nullptr) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -580,6 +594,25 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             }
 #endif
         }
+        if (REFLECT && hit && R.steps > 0 && (P.mat_flags[mat] & 7u) == 3u) {
+            // a reflective block (flags & 7 == 3) with budget left: undo the last crossing on the
+            // hit axis, mirror that axis (step and direction) and take the next DDA step from the
+            // block, as low_res.frag:170-189 + :319-331 do
+            const uint32_t ax = R.axis;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                if (ax == (uint32_t)k) {
+                    R.T[k] -= R.a(k);
+                    R.s[k] = -R.s[k];
+                    bounce->d[k] = -bounce->d[k];
+                }
+            }
+            bounce->n++;
+            dda_step(R);
+            hit = false;
+            done = false;
+            mat = 0u;
+        }
     }
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
@@ -619,11 +652,37 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     return h;
 }
 
-template <bool STATS, bool STAMPS, bool AO>
+// ------------------------------------------------------------------------------------------------
+// Shading: low_res.frag's colour model over castRayFromCam hits — sky
+// (genSkyBox :157-168), sun lighting (calcLightIntensity :242-252), 75-step shadow ray (:373-391),
+// the looked-at block highlight (:340-343) and reflections (:170-189, applied inside trace).
+// Single precision in the shader's operation order (-ffp-contract=off).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float3 color_of(uint64_t c) {  // color_int_to_vec3 (:139-145)
+    const double sc = 1.0 / 2097152.0;
+    return make_float3((float)((double)(c >> 42) * sc), (float)((double)((c >> 21) & 0x1FFFFFull) * sc),
+                       (float)((double)(c & 0x1FFFFFull) * sc));
+}
+
+__device__ __forceinline__ float sigmoidf(float x, float scale, float k) { return 1.0f / (1.0f + expf(-x * k)) * scale; }
+
+__device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]) {
+    float dy = d[1];
+    if (dy < 0.0f) dy *= 1.4f;
+    const float haze = (0.1f - fabsf(fminf(fmaxf(dy, -0.3f), 0.3f))) * 0.8f + 0.1f;
+    const float modifier = fminf(fmaxf(sigmoidf(1.0f - (haze * 2.0f), 1.0f, 2.0f), 0.0f), 1.0f);
+    const float ex = d[0] - sun[0], ey = dy - sun[1], ez = d[2] - sun[2];
+    const float b = sqrtf((ex * ex + ey * ey) + ez * ez) * 50.0f;
+    const float sv = sigmoidf(1.5f - b, 1.0f, 1.6f);
+    const float h3 = fminf(fmaxf(haze, 0.0f), 1.0f) * 3.0f;
+    return make_float3((0.2f + h3) * modifier + sv, (0.4f + h3) * modifier + sv, (1.0f + h3) * modifier + 0.0f);
+}
+
+template <bool STATS, bool STAMPS, bool AO, bool SHADE>
 #ifndef SVO_MIN_WAVES
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves)
-#define SVO_MIN_WAVES ((AO || STATS) ? 6 : 8)
+#define SVO_MIN_WAVES ((AO || STATS || SHADE) ? 6 : 8)
 #endif
 __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams P) {
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -695,7 +754,47 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         }
         out = 0;
     }
-    if (out >= 0) {
+    if (SHADE && out >= 0) {
+        Bounce bn = {{d[0], d[1], d[2]}, 0};
+        const Hit h = trace<false, true>(P, rsrc, path, o, d, P.steps, nullptr, &bn);
+        if (P.pos) {
+            reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
+            P.t[out] = h.t;
+            P.info[out] = h.info;
+        }
+        const bool hit = (h.info & HIT_BIT) != 0u;
+        float m = 1.0f;  // finalColorMod
+        for (int32_t i = 0; i < bn.n; i++) m *= 0.94f;
+        float3 c;
+        if (P.look_valid && h.x == P.look[0] && h.y == P.look[1] && h.z == P.look[2]) {
+            const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
+            c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
+        } else if (!hit) {
+            const float3 sk = sky_color(bn.d, P.sun);
+            c = make_float3(sk.x * m, sk.y * m, sk.z * m);
+        } else {
+            const float3 col = color_of(P.mat_color[h.info & MAT_MASK]);
+            const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
+            const int32_t sg = (h.info & NEG_BIT) ? -1 : 1;  // the ray's step on the hit axis
+            const float l = (ax == 0u ? P.sun[0] : (ax == 1u ? P.sun[1] : P.sun[2])) * (float)(-sg);
+            const bool facing = l > 0.0f;
+            const float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
+            c = make_float3(col.x * inten * m, col.y * inten * m, col.z * inten * m);
+            bool dark = false;
+            if (bn.n == 0) {
+                if (!facing) {
+                    dark = true;
+                } else {
+                    // shadow ray towards the sun from the centre of lastPos, through empty and liquid
+                    const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
+                                         (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
+                    dark = (trace<false>(P, rsrc, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
+                }
+            }
+            if (dark) c = make_float3(col.x * 0.3f * m, col.y * 0.3f * m, col.z * 0.3f * m);
+        }
+        P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
+    } else if (out >= 0) {
         const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
@@ -733,6 +832,9 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.mats = reinterpret_cast<const uint16_t*>(t->d_mats);
+    P.mat_color = reinterpret_cast<const uint64_t*>(t->d_pal);
+    P.mat_flags = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t->d_pal) +
+                                                    std::max<size_t>(t->palette.size(), 1) * 8);
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.steps = d->steps;
@@ -783,9 +885,10 @@ void svo::tree_release_device(svo_tree* t) {
     (void)hipSetDevice(t->device);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
     if (t->d_mats) (void)hipFree(t->d_mats);
+    if (t->d_pal) (void)hipFree(t->d_pal);
     if (t->d_work) (void)hipFree(t->d_work);
     (void)hipSetDevice(prev);
-    t->d_nodes = t->d_mats = t->d_work = nullptr;
+    t->d_nodes = t->d_mats = t->d_work = t->d_pal = nullptr;
     t->device = -1;
     t->device_bytes = 0;
 }
@@ -812,8 +915,17 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     HIP_TRY(hipMemcpy(t->d_nodes, t->nodes.data(), nb, hipMemcpyHostToDevice), SVO_EDEVICE);
     if (!t->mats.empty()) HIP_TRY(hipMemcpy(t->d_mats, t->mats.data(), t->mats.size() * sizeof(uint16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
+    // palette colours and flags for the shading pass
+    const size_t np = std::max<size_t>(t->palette.size(), 1);
+    std::vector<uint8_t> pal(np * 12, 0);
+    for (size_t i = 0; i < t->palette.size(); i++) {
+        memcpy(&pal[i * 8], &t->palette[i].color, 8);
+        memcpy(&pal[np * 8 + i * 4], &t->palette[i].flags, 4);
+    }
+    HIP_TRY(hipMalloc(&t->d_pal, pal.size()), SVO_ENOMEM);
+    HIP_TRY(hipMemcpy(t->d_pal, pal.data(), pal.size(), hipMemcpyHostToDevice), SVO_EDEVICE);
     t->device = device;
-    t->device_bytes = nb + mb + wb;
+    t->device_bytes = nb + mb + wb + pal.size();
     t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
     t->work_next = 0;
     return SVO_OK;
@@ -822,6 +934,40 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
 // ================================================================================================
 // casting
 // ================================================================================================
+extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const svo_shade_desc* sd, float* rgba,
+                              const svo_hits* o, void* stream) {
+    if (!t || !d || !sd || !rgba) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: NULL argument");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_shade_rays: tree not uploaded (svo_upload)");
+    if (d->steps < 0 || sd->shadow_steps < 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: negative step budget");
+    if (d->ao_samples != 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: AO is a separate pass (ao_samples must be 0)");
+    if (d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: no diagnostics in the shading pass");
+    if (o && (!o->pos_steps || !o->t || !o->info)) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: incomplete hit buffers");
+    if (d->ray_dirs) {
+        if (d->n_rays < 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: negative ray count");
+    } else if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0) {
+        SVO_FAIL(SVO_EINVAL, "svo_shade_rays: bad frame geometry");
+    }
+    const svo_hits none = {nullptr, nullptr, nullptr, nullptr};
+    CastParams P;
+    int64_t n = 0;
+    int rc = fill_params(t, d, o ? o : &none, P, n);
+    if (rc) return rc;
+    P.rgba = reinterpret_cast<float4*>(rgba);
+    for (int k = 0; k < 3; k++) {
+        P.sun[k] = sd->sun_dir[k];
+        P.look[k] = sd->look_at[k];
+    }
+    P.look_valid = sd->look_at_valid != 0;
+    P.shadow_steps = sd->shadow_steps;
+    if (n == 0) return SVO_OK;
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    const int64_t blocks = (n + kBlock - 1) / kBlock;
+    if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
+    hipLaunchKernelGGL((k_cast<false, false, false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+    return SVO_OK;
+}
+
 extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, void* stream) {
     if (!t || !d || !o) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL argument");
     if (!o->pos_steps || !o->t || !o->info) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL output buffer");
@@ -847,14 +993,14 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     const dim3 grid((uint32_t)blocks), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
     if (P.ao_n > 0) {
-        if (P.flags & SVO_CAST_STATS) hipLaunchKernelGGL((k_cast<true, true, true>), grid, block, 0, st, P);
-        else hipLaunchKernelGGL((k_cast<false, false, true>), grid, block, 0, st, P);
+        if (P.flags & SVO_CAST_STATS) hipLaunchKernelGGL((k_cast<true, true, true, false>), grid, block, 0, st, P);
+        else hipLaunchKernelGGL((k_cast<false, false, true, false>), grid, block, 0, st, P);
     } else if (P.flags & SVO_CAST_STATS) {
-        hipLaunchKernelGGL((k_cast<true, true, false>), grid, block, 0, st, P);
+        hipLaunchKernelGGL((k_cast<true, true, false, false>), grid, block, 0, st, P);
     } else if (P.flags & SVO_CAST_TIMELINE) {
-        hipLaunchKernelGGL((k_cast<false, true, false>), grid, block, 0, st, P);
+        hipLaunchKernelGGL((k_cast<false, true, false, false>), grid, block, 0, st, P);
     } else {
-        hipLaunchKernelGGL((k_cast<false, false, false>), grid, block, 0, st, P);
+        hipLaunchKernelGGL((k_cast<false, false, false, false>), grid, block, 0, st, P);
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
@@ -883,7 +1029,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL((k_cast<false, false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
+    hipLaunchKernelGGL((k_cast<false, false, false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);

@@ -47,6 +47,7 @@ struct svo_tree {
     void* d_nodes = nullptr;
     void* d_mats = nullptr;
     void* d_work = nullptr;   // scheduler counters (ring)
+    void* d_pal = nullptr;    // palette for shading: u64 colour[n] then u32 flags[n]
     uint32_t work_slots = 0;
     uint32_t work_next = 0;
     uint64_t device_bytes = 0;

@@ -93,3 +93,29 @@ def test_terrain_height_range(oracle_mod):
     r = facts()["terrain_4096_height_range"]
     h = oracle_mod.heights(4096, 4096)
     assert h.min() == r["min"] and h.max() == r["max"]
+
+
+def test_oracle_sky_matches_numpy_restatement(oracle_mod):
+    """oracle shading of rays that miss = genSkyBox (low_res.frag:157-168) restated in numpy float32"""
+    O = oracle_mod
+    t = O.Tree.reference_world()
+    sun = O.normalize((2.0, 1.0, 4.0))
+    W, H = 16, 9
+    cam = O.normalize((0.2, 1.0, 0.1))
+    rgba = t.shade_frame((50.0, 200.0, 50.0), cam, W, H, 300, sun)
+    f = np.float32
+    ppx, ppy = O.proj_plane(W, H)
+    np.seterr(over="ignore")  # exp(-x*k) may overflow to inf: the sigmoid is then 0, as in f32 C
+    for k in range(W * H):
+        d = np.array(O.pixel_dir(cam, ppx, ppy, W, H, k % W, k // W), f)
+        dy = d[1] * f(1.4) if d[1] < 0 else d[1]
+        haze = (f(0.1) - abs(min(max(dy, f(-0.3)), f(0.3)))) * f(0.8) + f(0.1)
+        sig = lambda x, s, kk: f(1.0) / (f(1.0) + np.exp(-x * f(kk), dtype=f)) * f(s)  # noqa: E731 (exp may overflow to inf: sigmoid -> 0)
+        modifier = min(max(sig(f(1.0) - haze * f(2.0), 1.0, 2.0), f(0)), f(1))
+        e = np.array([d[0] - sun[0], dy - sun[1], d[2] - sun[2]], f)
+        b = np.sqrt((e[0] * e[0] + e[1] * e[1]) + e[2] * e[2], dtype=f) * f(50.0)
+        sv = sig(f(1.5) - b, 1.0, 1.6)
+        h3 = min(max(haze, f(0)), f(1)) * f(3.0)
+        want = np.array([(f(0.2) + h3) * modifier + sv, (f(0.4) + h3) * modifier + sv, (f(1.0) + h3) * modifier], f)
+        assert np.allclose(rgba[k, :3], want, rtol=0, atol=2e-6), (k, rgba[k], want)
+        assert rgba[k, 3] == 0.0
