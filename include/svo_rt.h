@@ -119,8 +119,18 @@ int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32_t z, svo_b
 int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_t n, uint32_t* material_ids);
 /* copy the host image out (for tests / serialisation); byte sizes from svo_tree_get_info */
 int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nodes_bytes, void* mats, uint64_t mats_bytes);
-/* updateSsboData analogue: (re)upload the image to HBM of `device` */
+/* updateSsboData analogue: (re)upload the image to HBM of `device` (with room for edit blocks) */
 int svo_upload(svo_tree* t, int32_t device);
+/* Incremental edits: after putBlock / deleteBlock at `level` on the n positions
+   xyz of `w` (the world `t` was built from), patch `t` in place: each edited region's subtree is
+   re-linearised from `w` and its parent's child block rewritten at the end of the array (only
+   that parent's 16-B record changes in place).  The content equals a fresh svo_build of `w`; the
+   layout is not re-collapsed, and the tree is rebuilt from `w` when superseded blocks exceed half
+   of it.  Host only; svo_tree_sync brings the device copy up to date. */
+int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* xyz, int64_t n, int32_t level);
+/* upload what svo_tree_update changed: the appended tail and the rewritten records (or everything
+   after a rebuild / when the device allocation is outgrown) */
+int svo_tree_sync(svo_tree* t);
 void svo_tree_destroy(svo_tree* t);
 
 /* ---------------------------------------------------------------------------- casting ------- */

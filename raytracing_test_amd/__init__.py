@@ -122,7 +122,7 @@ ABI_SYMBOLS = (
     "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
-    "svo_build_heightfield", "svo_shade_rays",
+    "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
 )
 
 
@@ -160,6 +160,8 @@ def lib():
     L.svo_tree_get_block.argtypes = [vp, i32, i32, i32, C.POINTER(Block), C.POINTER(C.c_uint32)]
     L.svo_tree_export.argtypes = [vp, vp, C.c_uint64, vp, C.c_uint64]
     L.svo_upload.argtypes = [vp, i32]
+    L.svo_tree_update.argtypes = [vp, vp, vp, C.c_int64, i32]
+    L.svo_tree_sync.argtypes = [vp]
     L.svo_tree_destroy.argtypes = [vp]
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
@@ -389,6 +391,19 @@ class Tree:
         _check(lib().svo_tree_get_blocks(self._h, p.ctypes.data_as(C.c_void_p), len(p), ids.ctypes.data_as(C.c_void_p)),
                "svo_tree_get_blocks")
         return ids
+
+    def update(self, world, points, level=None):
+        """Incremental edits: patch this tree after world.put_block / delete_block at `level` on
+        `points` (svo_tree_update); then sync() to update the device copy."""
+        p = _xyz(points)
+        lv = self.info().levels + 1 if level is None else level
+        _check(lib().svo_tree_update(self._h, world._h, p.ctypes.data_as(C.c_void_p), len(p), lv), "svo_tree_update")
+        return self
+
+    def sync(self):
+        """Upload what update() changed (svo_tree_sync)."""
+        _check(lib().svo_tree_sync(self._h), "svo_tree_sync")
+        return self
 
     def export(self):
         i = self.info()

@@ -833,8 +833,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.mats = reinterpret_cast<const uint16_t*>(t->d_mats);
     P.mat_color = reinterpret_cast<const uint64_t*>(t->d_pal);
-    P.mat_flags = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t->d_pal) +
-                                                    std::max<size_t>(t->palette.size(), 1) * 8);
+    P.mat_flags = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t->d_pal) + t->dev_pal_n * 8);
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.steps = d->steps;
@@ -889,6 +888,7 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_work) (void)hipFree(t->d_work);
     (void)hipSetDevice(prev);
     t->d_nodes = t->d_mats = t->d_work = t->d_pal = nullptr;
+    t->dev_node_cap = t->dev_mat_cap = t->dev_pal_n = 0;
     t->device = -1;
     t->device_bytes = 0;
 }
@@ -899,6 +899,23 @@ extern "C" void svo_tree_destroy(svo_tree* t) {
     delete t;
 }
 
+static int upload_palette(svo_tree* t) {
+    // palette colours (u64[n]) then flags (u32[n]) for the shading pass
+    const size_t np = std::max<size_t>(t->palette.size(), 1);
+    std::vector<uint8_t> pal(np * 12, 0);
+    for (size_t i = 0; i < t->palette.size(); i++) {
+        memcpy(&pal[i * 8], &t->palette[i].color, 8);
+        memcpy(&pal[np * 8 + i * 4], &t->palette[i].flags, 4);
+    }
+    if (t->d_pal) (void)hipFree(t->d_pal);
+    t->d_pal = nullptr;
+    HIP_TRY(hipMalloc(&t->d_pal, pal.size()), SVO_ENOMEM);
+    HIP_TRY(hipMemcpy(t->d_pal, pal.data(), pal.size(), hipMemcpyHostToDevice), SVO_EDEVICE);
+    t->dev_pal_n = np;
+    t->palette_dirty = false;
+    return SVO_OK;
+}
+
 extern "C" int svo_upload(svo_tree* t, int32_t device) {
     if (!t) SVO_FAIL(SVO_EINVAL, "svo_upload: NULL tree");
     int ndev = 0;
@@ -906,28 +923,61 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     if (device < 0 || device >= ndev) SVO_FAIL(SVO_EDEVICE, "svo_upload: no such HIP device");
     tree_release_device(t);
     HIP_TRY(hipSetDevice(device), SVO_EDEVICE);
-    const size_t nb = t->nodes.size() * sizeof(Node);
-    const size_t mb = std::max<size_t>(t->mats.size() * sizeof(uint16_t), 16);
+    // capacity for appended edit blocks (svo_tree_update / svo_tree_sync) without reallocation
+    const uint64_t ncap = t->nodes.size() + t->nodes.size() / 8 + 65536;
+    const uint64_t mcap = t->mats.size() + t->mats.size() / 8 + 65536;
+    const size_t nb = ncap * sizeof(Node), mb = mcap * sizeof(uint16_t);
     const size_t wb = 4096;
     HIP_TRY(hipMalloc(&t->d_nodes, nb), SVO_ENOMEM);
     HIP_TRY(hipMalloc(&t->d_mats, mb), SVO_ENOMEM);
     HIP_TRY(hipMalloc(&t->d_work, wb), SVO_ENOMEM);
-    HIP_TRY(hipMemcpy(t->d_nodes, t->nodes.data(), nb, hipMemcpyHostToDevice), SVO_EDEVICE);
+    HIP_TRY(hipMemcpy(t->d_nodes, t->nodes.data(), t->nodes.size() * sizeof(Node), hipMemcpyHostToDevice), SVO_EDEVICE);
     if (!t->mats.empty()) HIP_TRY(hipMemcpy(t->d_mats, t->mats.data(), t->mats.size() * sizeof(uint16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
-    // palette colours and flags for the shading pass
-    const size_t np = std::max<size_t>(t->palette.size(), 1);
-    std::vector<uint8_t> pal(np * 12, 0);
-    for (size_t i = 0; i < t->palette.size(); i++) {
-        memcpy(&pal[i * 8], &t->palette[i].color, 8);
-        memcpy(&pal[np * 8 + i * 4], &t->palette[i].flags, 4);
-    }
-    HIP_TRY(hipMalloc(&t->d_pal, pal.size()), SVO_ENOMEM);
-    HIP_TRY(hipMemcpy(t->d_pal, pal.data(), pal.size(), hipMemcpyHostToDevice), SVO_EDEVICE);
+    int rc = upload_palette(t);
+    if (rc) return rc;
     t->device = device;
-    t->device_bytes = nb + mb + wb + pal.size();
+    t->device_bytes = nb + mb + wb + t->dev_pal_n * 12;
     t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
     t->work_next = 0;
+    t->dev_node_cap = ncap;
+    t->dev_mat_cap = mcap;
+    t->synced_nodes = t->nodes.size();
+    t->synced_mats = t->mats.size();
+    t->dirty_nodes.clear();
+    t->full_upload = false;
+    return SVO_OK;
+}
+
+// updateSsboData after edits (voxel_allocator.hpp:38-78): only the appended tail and the records
+// rewritten in place travel; a rebuilt or outgrown tree is uploaded whole
+extern "C" int svo_tree_sync(svo_tree* t) {
+    if (!t) SVO_FAIL(SVO_EINVAL, "svo_tree_sync: NULL tree");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_sync: tree not uploaded (svo_upload)");
+    if (t->full_upload || t->nodes.size() > t->dev_node_cap || t->mats.size() > t->dev_mat_cap) return svo_upload(t, t->device);
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    Node* dn = reinterpret_cast<Node*>(t->d_nodes);
+    if (t->nodes.size() > t->synced_nodes)
+        HIP_TRY(hipMemcpy(dn + t->synced_nodes, t->nodes.data() + t->synced_nodes, (t->nodes.size() - t->synced_nodes) * sizeof(Node),
+                          hipMemcpyHostToDevice), SVO_EDEVICE);
+    if (t->mats.size() > t->synced_mats)
+        HIP_TRY(hipMemcpy(reinterpret_cast<uint16_t*>(t->d_mats) + t->synced_mats, t->mats.data() + t->synced_mats,
+                          (t->mats.size() - t->synced_mats) * sizeof(uint16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    std::sort(t->dirty_nodes.begin(), t->dirty_nodes.end());
+    for (size_t i = 0; i < t->dirty_nodes.size();) {  // runs of consecutive rewritten records
+        size_t j = i + 1;
+        while (j < t->dirty_nodes.size() && t->dirty_nodes[j] <= t->dirty_nodes[j - 1] + 1) j++;
+        const uint32_t lo = t->dirty_nodes[i], hi = t->dirty_nodes[j - 1];
+        HIP_TRY(hipMemcpy(dn + lo, t->nodes.data() + lo, (size_t)(hi - lo + 1) * sizeof(Node), hipMemcpyHostToDevice), SVO_EDEVICE);
+        i = j;
+    }
+    if (t->palette_dirty) {
+        int rc = upload_palette(t);
+        if (rc) return rc;
+    }
+    t->dirty_nodes.clear();
+    t->synced_nodes = t->nodes.size();
+    t->synced_mats = t->mats.size();
     return SVO_OK;
 }
 

@@ -51,6 +51,13 @@ struct svo_tree {
     uint32_t work_slots = 0;
     uint32_t work_next = 0;
     uint64_t device_bytes = 0;
+    // incremental edits (svo_tree_update in svo_world.cpp, svo_tree_sync in svo_cast.hip): changed
+    // node blocks are appended; superseded ones are garbage until the next full rebuild
+    uint64_t garbage_nodes = 0, garbage_mats = 0;
+    uint64_t synced_nodes = 0, synced_mats = 0;  // prefix of nodes / mats already in HBM
+    std::vector<uint32_t> dirty_nodes;           // rewritten in place below synced_nodes
+    bool palette_dirty = false, full_upload = false;
+    uint64_t dev_node_cap = 0, dev_mat_cap = 0, dev_pal_n = 0;  // device allocations (elements)
 };
 
 namespace svo {

@@ -12,7 +12,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <deque>
 #include <functional>
+#include <unordered_map>
 #include <map>
 #include <thread>
 #include <vector>
@@ -460,6 +462,181 @@ extern "C" int svo_build(const svo_world* w, svo_tree** out) {
     }
     finish_tree_stats(t);
     *out = t;
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Incremental edits (putBlock / deleteBlock + updateSsboData,
+// voxel_allocator.hpp:38-78).  After world edits, the linearised tree is patched instead of
+// rebuilt: for each edited region, the deepest interior node A above it whose subtree still holds
+// the old content is found; the edited child of A is re-linearised from the world (its subtree
+// appended breadth-first), and A's child block is rewritten at the end of the array with the new
+// child record (siblings are copied: their own subtrees stay where they are).  Only A's record is
+// changed in place.  Results are the tree's *content*, not its canonical layout: regions that
+// become uniform are not re-collapsed (traversal is unaffected); when superseded blocks exceed
+// half the array, the tree is rebuilt from the world.  svo_tree_sync uploads the appended tail
+// and the rewritten records.
+// ================================================================================================
+namespace {
+struct Emitter {
+    svo_tree* t;
+    const svo_world* w;
+    std::vector<uint8_t> solid;
+    std::unordered_map<uint32_t, uint32_t> cls;  // classes of the world nodes visited
+
+    uint32_t classify(uint32_t n) {
+        auto it = cls.find(n);
+        if (it != cls.end()) return it->second;
+        const auto& e = w->nodes[n];
+        uint32_t c;
+        if (e.leaf) {
+            c = solid[e.mat] ? (uint32_t)e.mat : C_EMPTY;
+        } else {
+            uint32_t kc[64];
+            const uint32_t* k = w->kids(n);
+            for (int i = 0; i < 64; i++) kc[i] = k[i] ? classify(k[i]) : C_EMPTY;
+            c = fold_classes(kc);
+        }
+        cls[n] = c;
+        return c;
+    }
+
+    // record of world node e at depth d; its descendants are appended breadth-first.  The record
+    // is written to *root_rec (index -1) or t->nodes[idx].
+    Node emit(uint32_t e, int d) {
+        const int L = t->levels;
+        struct Item {
+            uint32_t e;
+            int d;
+            int64_t idx;
+        };
+        std::deque<Item> q;
+        q.push_back({e, d, -1});
+        Node root_rec{0, 0, K_INTERIOR};
+        while (!q.empty()) {
+            const Item it = q.front();
+            q.pop_front();
+            const uint32_t c = classify(it.e);
+            Node rec{0, 0, K_INTERIOR};
+            if (c == C_MIXED) {
+                const uint32_t* k = w->kids(it.e);
+                if (it.d == L - 1) {
+                    uint32_t vox[64];
+                    for (int v = 0; v < 64; v++) vox[v] = k[v] ? classify(k[v]) : C_EMPTY;
+                    const uint32_t ref = (uint32_t)t->mats.size();
+                    BrickOut b = make_brick(vox, &t->mats);
+                    rec = Node{b.mask, (b.info & K_UNIFORM) ? 0u : ref, b.info};
+                } else {
+                    uint64_t mask = 0;
+                    for (int sl = 0; sl < 64; sl++)
+                        if (k[sl] && classify(k[sl]) != C_EMPTY) mask |= 1ull << sl;
+                    const uint64_t base = t->nodes.size();
+                    t->nodes.resize(base + __builtin_popcountll(mask), Node{0, 0, 0});
+                    int64_t j = (int64_t)base;
+                    for (int sl = 0; sl < 64; sl++)
+                        if ((mask >> sl) & 1ull) q.push_back({k[sl], it.d + 1, j++});
+                    rec = Node{mask, (uint32_t)base, K_INTERIOR};
+                }
+            } else if (c != C_EMPTY) {
+                rec = Node{~0ull, 0, K_SOLID | (c << 16)};
+            }
+            if (it.idx < 0) root_rec = rec;
+            else t->nodes[(size_t)it.idx] = rec;
+        }
+        return root_rec;
+    }
+};
+
+// class of the world region of depth `d` holding (x, y, z): its node, or a uniform class when a
+// leaf above covers it / nothing is stored there
+struct WorldRegion {
+    bool has_node;
+    uint32_t node;
+    uint32_t cls;
+};
+WorldRegion world_region(const svo_world* w, const std::vector<uint8_t>& solid, uint32_t x, uint32_t y, uint32_t z, int d) {
+    uint32_t n = 0;
+    for (int depth = 0;; depth++) {
+        const auto& e = w->nodes[n];
+        if (e.leaf) return {false, 0, solid[e.mat] ? (uint32_t)e.mat : C_EMPTY};
+        if (depth == d) return {true, n, 0};
+        const uint32_t c = w->kids(n)[child_slot(x, y, z, (uint32_t)(2 * (w->levels - 1 - depth)))];
+        if (!c) return {false, 0, C_EMPTY};
+        n = c;
+    }
+}
+}  // namespace
+
+extern "C" int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* xyz, int64_t n, int32_t level) {
+    if (!t || !w || (!xyz && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_tree_update: NULL argument");
+    if (t->levels != w->levels) SVO_FAIL(SVO_EINVAL, "svo_tree_update: tree and world differ in levels");
+    if (level < 1 || level > w->levels + 1) SVO_FAIL(SVO_EINVAL, "svo_tree_update: level out of range");
+    const int L = t->levels;
+    const int de = level - 1;  // depth of the edited region (putBlock's `level--`)
+    if (w->pal.m.size() != t->palette.size()) {
+        t->palette = w->pal.m;  // the world's palette only grows: ids stay valid
+        t->palette_dirty = true;
+    }
+    Emitter em{t, w, std::vector<uint8_t>(w->pal.m.size()), {}};
+    for (size_t i = 0; i < em.solid.size(); i++) em.solid[i] = material_solid(w->pal.m[i]);
+    const uint32_t mk = (1u << (2 * L)) - 1u;
+    bool rebuild = de == 0 || node_kind(t->nodes[0].info) != K_INTERIOR;
+    for (int64_t i = 0; i < n && !rebuild; i++) {
+        const uint32_t x = (uint32_t)xyz[3 * i] & mk, y = (uint32_t)xyz[3 * i + 1] & mk, z = (uint32_t)xyz[3 * i + 2] & mk;
+        // A: the deepest interior node above the edited region whose child on the path is interior
+        uint32_t a = 0;
+        int da = 0;
+        while (da < de - 1) {
+            const Node& A = t->nodes[a];
+            const uint32_t sl = child_slot(x, y, z, (uint32_t)(2 * (L - 1 - da)));
+            if (!((A.mask >> sl) & 1ull)) break;
+            const uint32_t ci = A.ref + (uint32_t)__builtin_popcountll(A.mask & ((1ull << sl) - 1ull));
+            if (node_kind(t->nodes[ci].info) != K_INTERIOR) break;
+            a = ci;
+            da++;
+        }
+        // the child of A on the path, re-linearised from the world
+        const uint32_t s = child_slot(x, y, z, (uint32_t)(2 * (L - 1 - da)));
+        const WorldRegion r = world_region(w, em.solid, x, y, z, da + 1);
+        Node rec{0, 0, K_INTERIOR};
+        bool empty;
+        if (r.has_node) {
+            empty = em.classify(r.node) == C_EMPTY;
+            if (!empty) rec = em.emit(r.node, da + 1);
+        } else {
+            empty = r.cls == C_EMPTY;
+            if (!empty) rec = Node{~0ull, 0, K_SOLID | (r.cls << 16)};
+        }
+        // A's child block, rewritten at the end of the array
+        const Node A = t->nodes[a];
+        const uint64_t m_old = A.mask, m_new = empty ? (m_old & ~(1ull << s)) : (m_old | (1ull << s));
+        const uint64_t base = t->nodes.size();
+        t->nodes.resize(base + __builtin_popcountll(m_new));
+        uint64_t j = base;
+        for (uint32_t sl = 0; sl < 64; sl++) {
+            if (!((m_new >> sl) & 1ull)) continue;
+            t->nodes[j++] = sl == s ? rec : t->nodes[A.ref + (uint32_t)__builtin_popcountll(m_old & ((1ull << sl) - 1ull))];
+        }
+        t->garbage_nodes += (uint64_t)__builtin_popcountll(m_old);
+        t->nodes[a] = Node{m_new, (uint32_t)base, K_INTERIOR};
+        if (a < t->synced_nodes) t->dirty_nodes.push_back(a);
+        em.cls.clear();  // the next edit may change classes on its own path
+        if (t->nodes.size() > 0xFFFFFFFFull) rebuild = true;
+    }
+    if (rebuild || t->garbage_nodes * 2 > t->nodes.size()) {
+        svo_tree* f = nullptr;
+        int rc = svo_build(w, &f);
+        if (rc) return rc;
+        t->nodes.swap(f->nodes);
+        t->mats.swap(f->mats);
+        t->palette.swap(f->palette);
+        for (int i = 0; i < 8; i++) t->nodes_per_level[i] = f->nodes_per_level[i];
+        t->n_bricks = f->n_bricks;
+        t->garbage_nodes = t->garbage_mats = 0;
+        t->dirty_nodes.clear();
+        t->full_upload = t->palette_dirty = true;
+        delete f;
+    }
     return SVO_OK;
 }
 

@@ -1,0 +1,68 @@
+"""Incremental edits on the GPU: after world edits, svo_tree_update + svo_tree_sync
+must give the same casts as a freshly built and uploaded tree (bit-exact hit records)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _frames_equal(rt, a, b, label):
+    ga, gb = rt.decode_hits(a), rt.decode_hits(b)
+    for k in ("pos", "steps", "hit", "material", "axis"):
+        assert np.array_equal(ga[k], gb[k]), "%s: %s differs at %d rays" % (label, k, int((ga[k] != gb[k]).reshape(len(ga[k]), -1).any(1).sum()))
+    assert np.array_equal(ga["t"].view(np.uint32), gb["t"].view(np.uint32)), label
+
+
+def test_edits_then_sync_match_fresh_upload(rt, torch_cuda):
+    rng = np.random.default_rng(21)
+    w = rt.World.reference()
+    tree = w.build().upload(0)
+    cams = [((35.0, 50.0, 35.0), (1.0, 0.0, 1.0)), ((4.0, 90.0, 4.0), (1.0, -0.45, 1.0))]
+    for step in range(4):
+        # carve the terrain in view, drop blocks (some reflective) in the sky, fill a 4^3 block
+        carve = np.stack([rng.integers(30, 120, 80), rng.integers(20, 50, 80), rng.integers(30, 120, 80)], 1)
+        for p in carve:
+            w.delete_block(*[int(v) for v in p])
+        tree.update(w, carve)
+        sky = np.stack([rng.integers(20, 150, 40), rng.integers(50, 90, 40), rng.integers(20, 150, 40)], 1)
+        w.put_blocks(sky, rng.choice([0, 2], size=len(sky)).astype(np.uint32), rng.integers(1, 1 << 60, len(sky)).astype(np.uint64))
+        tree.update(w, sky)
+        blk = np.array([[60 + 8 * step, 40, 60]])
+        w.put_blocks(blk, np.zeros(1, np.uint32), np.full(1, 4242, np.uint64), level=w.levels)
+        tree.update(w, blk, level=w.levels)
+        tree.sync()
+        fresh = w.build().upload(0)
+        for ci, (org, cd) in enumerate(cams):
+            cam = rt.normalize(cd)
+            for S in (30, 300):
+                _frames_equal(rt, tree.cast_frame(org, cam, 480, 270, S), fresh.cast_frame(org, cam, 480, 270, S),
+                              "step %d cam %d S=%d" % (step, ci, S))
+        a = tree.shade_frame(cams[0][0], rt.normalize(cams[0][1]), 240, 136, 300, sun=rt.sun_dir())
+        b = fresh.shade_frame(cams[0][0], rt.normalize(cams[0][1]), 240, 136, 300, sun=rt.sun_dir())
+        assert torch_cuda.equal(a, b)
+
+
+def test_sync_after_rebuild_and_growth(rt, torch_cuda):
+    """many edits on a small world: the tree is rebuilt / outgrows its device allocation; sync re-uploads"""
+    rng = np.random.default_rng(2)
+    w = rt.World(levels=4)
+    w.put_block(10, 10, 10, 0, 3)
+    tree = w.build().upload(0)
+    for _ in range(20):
+        pts = rng.integers(0, 256, size=(200, 3))
+        w.put_blocks(pts, np.zeros(len(pts), np.uint32), rng.integers(1, 50, len(pts)).astype(np.uint64))
+        tree.update(w, pts)
+        tree.sync()
+    fresh = w.build().upload(0)
+    cam = rt.normalize((1.0, -0.3, 0.7))
+    _frames_equal(rt, tree.cast_frame((-20.5, 180.0, -10.0), cam, 256, 144, 600), fresh.cast_frame((-20.5, 180.0, -10.0), cam, 256, 144, 600),
+                  "growth")
