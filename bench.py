@@ -110,6 +110,7 @@ def main():
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
     ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
+    ap.add_argument("--host-build", action="store_true", help="build the tree on the host (default: svo_build_terrain_gpu)")
     ap.add_argument("--shade", action="store_true",
                     help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray), "
                          "rgba gathered instead of hit records")
@@ -139,9 +140,13 @@ def main():
     if args.cols is None:
         args.cols = 4096 if args.config == "c3" else 16384
     t0 = time.time()
-    tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
-    build_s = time.time() - t0
-    tree.upload(dev)
+    if args.host_build:
+        tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
+        build_s = time.time() - t0
+        tree.upload(dev)
+    else:  # noise + build in HBM (identical arrays, tests/test_gpu_build.py); already uploaded
+        tree = rt.Tree.terrain_gpu(LEVELS, args.cols, args.cols, dev)
+        build_s = time.time() - t0
     info = tree.info()
     ppx, ppy = rt.proj_plane(W, H)
     cam = rt.normalize(CAM)
@@ -284,7 +289,8 @@ def main():
                    " primary rays per GPU per step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % STEPS,
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
                    "gather": world > 1 and not args.no_gather, "tree_nodes": info.n_nodes,
-                   "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 2)},
+                   "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
+                   "tree_builder": "host" if args.host_build else "gpu"},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

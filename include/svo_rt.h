@@ -110,6 +110,12 @@ int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nth
 /* the same builder from caller-given column tops heights[x*length + z] (0 <= h <= extent-2) */
 int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t nthreads,
                           svo_tree** out);
+/* The same two builders on the GPU: noise per column, min/max pyramid and a
+   level-synchronous breadth-first build in HBM (one wavefront per region, ballots + scans).  The
+   node / material arrays equal svo_build_terrain's byte for byte; the tree comes back already
+   uploaded to `device` (plus its host image). */
+int svo_build_terrain_gpu(int32_t levels, int32_t width, int32_t length, int32_t device, svo_tree** out);
+int svo_build_heightfield_gpu(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t device, svo_tree** out);
 int svo_tree_get_info(const svo_tree* t, svo_tree_info* out);
 /* palette entry `id` (id 0 = empty block) */
 int svo_tree_palette(const svo_tree* t, uint32_t id, svo_block* out);

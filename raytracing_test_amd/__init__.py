@@ -123,6 +123,7 @@ ABI_SYMBOLS = (
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
+    "svo_build_terrain_gpu", "svo_build_heightfield_gpu",
 )
 
 
@@ -181,6 +182,8 @@ def lib():
     L.svo_hemisphere.argtypes = [i32, vp]
     L.svo_gen_heightfield.argtypes = [vp, i32, i32, vp]
     L.svo_build_heightfield.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
+    L.svo_build_terrain_gpu.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
+    L.svo_build_heightfield_gpu.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
     _lib = L
     return L
 
@@ -364,6 +367,21 @@ class Tree:
         t = C.c_void_p()
         _check(lib().svo_build_heightfield(levels, h.shape[0], h.shape[1], h.ctypes.data_as(C.c_void_p), nthreads, C.byref(t)),
                "svo_build_heightfield")
+        return cls(t)
+
+    @classmethod
+    def terrain_gpu(cls, levels, width, length, device=0):
+        """svo_build_terrain on the GPU (noise + build in HBM): the tree comes back uploaded to `device`."""
+        h = C.c_void_p()
+        _check(lib().svo_build_terrain_gpu(levels, width, length, device, C.byref(h)), "svo_build_terrain_gpu")
+        return cls(h)
+
+    @classmethod
+    def heightfield_gpu(cls, levels, heights, device=0):
+        h = np.ascontiguousarray(heights, np.int32)
+        t = C.c_void_p()
+        _check(lib().svo_build_heightfield_gpu(levels, h.shape[0], h.shape[1], h.ctypes.data_as(C.c_void_p), device, C.byref(t)),
+               "svo_build_heightfield_gpu")
         return cls(t)
 
     def info(self):

@@ -15,8 +15,8 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("SVO_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["svo_world.cpp"]
-HIP_SRCS = ["svo_cast.hip"]
-HEADERS = ["svo_common.h", "svo_noise.h", "svo_internal.h"]
+HIP_SRCS = ["svo_cast.hip", "svo_build.hip"]
+HEADERS = ["svo_common.h", "svo_noise.h", "svo_internal.h", "svo_hip.h"]
 
 
 def _newer(target, deps):

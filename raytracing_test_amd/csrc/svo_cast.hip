@@ -16,24 +16,10 @@
 #include <string>
 
 #include "../../include/svo_rt.h"
+#include "svo_hip.h"
 #include "svo_internal.h"
 
 using namespace svo;
-
-#define SVO_FAIL(code, msg)     \
-    do {                        \
-        svo::set_error(msg);    \
-        return (code);          \
-    } while (0)
-
-#define HIP_TRY(expr, code)                                                                    \
-    do {                                                                                       \
-        hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess) {                                                                \
-            svo::set_error(std::string(#expr " failed: ") + hipGetErrorString(e_));            \
-            return (code);                                                                     \
-        }                                                                                      \
-    } while (0)
 
 namespace {
 
@@ -942,6 +928,29 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     t->work_next = 0;
     t->dev_node_cap = ncap;
     t->dev_mat_cap = mcap;
+    t->synced_nodes = t->nodes.size();
+    t->synced_mats = t->mats.size();
+    t->dirty_nodes.clear();
+    t->full_upload = false;
+    return SVO_OK;
+}
+
+int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_cap, void* d_mats, uint64_t mat_cap) {
+    tree_release_device(t);
+    HIP_TRY(hipSetDevice(device), SVO_EDEVICE);
+    const size_t wb = 4096;
+    t->d_nodes = d_nodes;
+    t->d_mats = d_mats;
+    HIP_TRY(hipMalloc(&t->d_work, wb), SVO_ENOMEM);
+    HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
+    int rc = upload_palette(t);
+    if (rc) return rc;
+    t->device = device;
+    t->device_bytes = node_cap * sizeof(Node) + mat_cap * sizeof(uint16_t) + wb + t->dev_pal_n * 12;
+    t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
+    t->work_next = 0;
+    t->dev_node_cap = node_cap;
+    t->dev_mat_cap = mat_cap;
     t->synced_nodes = t->nodes.size();
     t->synced_mats = t->mats.size();
     t->dirty_nodes.clear();

@@ -62,4 +62,7 @@ struct svo_tree {
 
 namespace svo {
 void tree_release_device(svo_tree* t);  // svo_cast.hip
+// take over device arrays built on `device` (node_cap / mat_cap elements allocated, the host image
+// already equal to their first nodes.size() / mats.size() elements): svo_cast.hip
+int adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_cap, void* d_mats, uint64_t mat_cap);
 }
