@@ -217,16 +217,12 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 }
 
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
-// leave the box.  Returns false (state unchanged) when the budget ends inside the box.
-// #{ j >= 0 : T + j*a < W }, exact under exact_axis.  k0 = trunc((W-T)/a) from an f32 estimate (error < 1 for counts below 2^20) is at
-// most 2 below the count; the monotone tests T + k0*a < W and T + (k0+1)*a < W (both values exact
-// on the ray's grid) add the rest.
+// #{ j >= 0 : T + j*a < W } = c, exact under exact_axis.  The f32 estimate q ~ (W-T)/a is within
+// 1/4 of the truth for counts below 2^20 (relative error < 2^-22), so m = floor(q + 1/2), clamped
+// at 0, is c-1 or c, and one exact test on the ray's grid decides: c = m + [T + m*a < W].
 __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, double W) {
-    const float q = (float)(W - T) * inva;
-    const int32_t k0 = (int32_t)fmaxf(q, 0.0f);
-    const double X = on_grid(T, k0, a);
-    const double X1 = X + a;
-    return k0 + (int32_t)(X < W) + (int32_t)(X1 < W);
+    const int32_t m = (int32_t)fmaxf(__builtin_fmaf((float)(W - T), inva, 0.5f), 0.0f);
+    return m + (int32_t)(on_grid(T, m, a) < W);
 }
 
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
@@ -446,8 +442,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    // budget < 2^21 also keeps the f32 count estimates within 1 of the truth (count_lt_w)
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 21) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
+    // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_lt_w)
+    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
                       exact_axis(R.T[2], R.a(2), budget);
     bool hit = false;
     uint32_t mat = 0u;
