@@ -68,6 +68,9 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #ifndef SVO_BRICK_FAST
 #define SVO_BRICK_FAST 1
 #endif
+#ifndef SVO_UNIFORM_DIRS
+#define SVO_UNIFORM_DIRS 1
+#endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
@@ -169,10 +172,20 @@ __device__ __forceinline__ void dda_step(Ray& R) {
 
 // Free slots of a 4-slot line (bit = occupied) beyond slot c in the step direction, before an
 // occupied slot or the end of the line.  Branch-free.
+__device__ __forceinline__ uint32_t run_up(uint32_t occ, uint32_t c) {
+    return (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
+}
+__device__ __forceinline__ uint32_t run_down(uint32_t occ, uint32_t c) {
+    return c - (32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u))));
+}
+// the wave's rays nearly always share their step signs: one variant on a wave-uniform branch
 __device__ __forceinline__ uint32_t run_fwd(uint32_t occ, uint32_t c, bool pos) {
-    const uint32_t up = (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
-    const uint32_t down = c - (32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u))));
-    return pos ? up : down;
+#if SVO_UNIFORM_DIRS
+    const uint64_t b = __ballot(pos);
+    if (b == __builtin_amdgcn_read_exec()) return run_up(occ, c);
+    if (b == 0ull) return run_down(occ, c);
+#endif
+    return pos ? run_up(occ, c) : run_down(occ, c);
 }
 
 // slots c .. c+n (pos) or c-n .. c of a 4-slot line
