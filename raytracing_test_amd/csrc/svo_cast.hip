@@ -71,6 +71,9 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #ifndef SVO_UNIFORM_DIRS
 #define SVO_UNIFORM_DIRS 1
 #endif
+#ifndef SVO_BRICK_PACK
+#define SVO_BRICK_PACK 1
+#endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
@@ -433,6 +436,37 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 template <bool STATS, bool TLAST>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
+#if SVO_BRICK_PACK
+    // steps left (bytes 0-2) and voxel index (byte 3) in one register: one select + add per step
+    uint32_t pk = left0 | (child_slot(w[0], w[1], w[2], 0u) << 24);
+    const uint32_t d0 = ((uint32_t)R.s[0] << 24) - 1u, d1 = ((uint32_t)(R.s[1] * 4) << 24) - 0x100u,
+                   d2 = ((uint32_t)(R.s[2] * 16) << 24) - 0x10000u;
+    bool go;
+    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
+        solid = (bmask >> (pk >> 24)) & 1ull;
+        go = !solid && R.steps > 0;
+        if (go) {
+            // one DDA step (ray_caster.cpp:70-80) without position updates
+            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+            const bool cy = !cx && (R.T[1] < R.T[2]);
+            const bool cz = !cx && !cy;
+            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            R.axis = cx ? 0u : (cy ? 1u : 2u);
+            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+            R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
+            R.steps--;
+            pk += cx ? d0 : (cy ? d1 : d2);
+            if (STATS) {
+                st.brick_steps++;
+                st.wv_brick += wave_lead();
+            }
+            go = ((pk - 0x010101u) & ~pk & 0x808080u) == 0u;  // no byte at 0: still inside
+        }
+    } while (go);
+    left = pk & 0xFFFFFFu;
+    return pk >> 24;
+#else
     uint32_t v = child_slot(w[0], w[1], w[2], 0u);
     const int32_t dvx = R.s[0], dvy = R.s[1] * 4, dvz = R.s[2] * 16;
     left = left0;
@@ -461,6 +495,7 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
         }
     } while (go);
     return v;
+#endif
 }
 
 // Reflections of the shading pass (reflectRay, low_res.frag:170-189): direction after them and count.
@@ -575,9 +610,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             const int32_t nx = (int32_t)((left0 & 0xFFu) - (left & 0xFFu));
             const int32_t ny = (int32_t)(((left0 >> 8) & 0xFFu) - ((left >> 8) & 0xFFu));
             const int32_t nz = (int32_t)((left0 >> 16) - (left >> 16));
-            R.r[0] += R.s[0] > 0 ? nx : -nx;
-            R.r[1] += R.s[1] > 0 ? ny : -ny;
-            R.r[2] += R.s[2] > 0 ? nz : -nz;
+            R.r[0] += __mul24(R.s[0], nx);
+            R.r[1] += __mul24(R.s[1], ny);
+            R.r[2] += __mul24(R.s[2], nz);
 #else
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
