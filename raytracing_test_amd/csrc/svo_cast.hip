@@ -327,7 +327,6 @@ struct Parent {
     uint64_t mask;
     uint32_t ref;
     uint32_t sh;  // child shift: a child region is 2^sh voxels wide, the parent's 2^(sh+2)
-    uint32_t w[3];
     bool valid;
 };
 
@@ -344,13 +343,15 @@ __device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uin
 
 template <bool STATS>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
-                                           const uint32_t w[3], Parent& par, uint32_t& sh_out, uint64_t& bmask,
+                                           const uint32_t w[3], uint32_t moved, Parent& par, uint32_t& sh_out, uint64_t& bmask,
                                            uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
     if (par.valid) {
-        const uint32_t diff = (w[0] ^ par.w[0]) | (w[1] ^ par.w[1]) | (w[2] ^ par.w[2]);
+        // the previous voxel lies in the parent's region (every move starts inside it), so the
+        // bits in which the last step changed the stepped coordinate tell whether the ray left it
+        const uint32_t diff = moved;
         if ((diff >> (par.sh + 2u)) != 0u) {
             // left the parent's region: the deepest node of the last descent whose region also
             // holds this cell (depth levels-1-floor(h/2), h = highest differing bit) becomes the
@@ -359,9 +360,6 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             par.mask = path.mask[da * kBlock];
             par.ref = path.ref[da * kBlock];
             par.sh = (uint32_t)(2 * (P.levels - 1 - da));
-            par.w[0] = w[0];
-            par.w[1] = w[1];
-            par.w[2] = w[2];
             if (STATS) st.path_starts++;
         }
         const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
@@ -392,9 +390,6 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             par.mask = n.mask;
             par.ref = n.ref;
             par.sh = sh;
-            par.w[0] = w[0];
-            par.w[1] = w[1];
-            par.w[2] = w[2];
             par.valid = true;
             const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
             const bool occ = (n.mask >> sl) & 1ull;
@@ -537,7 +532,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     Parent par;
     par.valid = false;
     par.mask = 0ull;
-    par.ref = par.sh = par.w[0] = par.w[1] = par.w[2] = 0u;
+    par.ref = par.sh = 0u;
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
@@ -550,7 +545,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         uint32_t w[3];
         wrap3(R, wm, w);
         uint32_t sh = 0u;
-        const uint32_t kind = lookup<STATS>(P, rsrc, path, w, par, sh, bmask, bref, binfo, st);
+        const uint32_t ax = R.axis;
+        const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
+        const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
+        const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
+        const uint32_t kind = lookup<STATS>(P, rsrc, path, w, moved, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
             hit = true;
             mat = binfo >> 16;
