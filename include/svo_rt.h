@@ -223,9 +223,11 @@ int svo_sync(void* hip_stream);
      look_at voxel   -> colour x 2 + 0.3 (:340-343)
    A block with flags & 7 == 3 reflects the ray while budget remains (:170-189, :319-331):
    the last crossing on the hit axis is undone, that axis's step and direction flip, the DDA
-   continues; finalColorMod *= 0.94 per reflection.  Refraction (flags & 7 == 5) is not modelled:
-   liquid passes (castRayFromCam), refractive solids shade as opaque.  Single precision in the
-   shader's operation order. */
+   continues; finalColorMod *= 0.94 per reflection.  A refractive solid (flags & 7 == 5, not
+   liquid) while budget remains is passed with finalColorMod *= 0.95; the first one bends the ray
+   (refractRay :196-240, n 1.0 -> 1.1, normal = hit axis x step, the shader's origin-based exact
+   position) and deltaPos restarts from the current cell.  Liquid passes unbent (it is empty in
+   castRayFromCam and in the tree).  Single precision in the shader's operation order. */
 typedef struct {
     float sun_dir[3];      /* normalised sunDir (globals.cpp:23: normalize(2,1,4)) */
     int32_t look_at[3];    /* lookingAtBlock (main.cpp:81,89) */

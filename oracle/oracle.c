@@ -1205,15 +1205,39 @@ EXPORT void orc_cast_frame_ao(const otree* t, const float org[3], const float ca
 /* ------------------------------------------------------------------------------------------------
  * Shading, restating include/svo_rt.h's svo_shade_rays contract: low_res.frag's
  * colour model (genSkyBox :157-168, calcLightIntensity :242-252, shadow ray :373-391, highlight
- * :340-343, reflectRay :170-189) over castRayFromCam hits.  Single precision, shader op order.
+ * :340-343, reflectRay :170-189, refractRay :196-240 for non-liquid blocks) over castRayFromCam hits.  Single precision, shader op order.
  * ---------------------------------------------------------------------------------------------- */
-/* o_cast with reflections: a hit on a block with (flags & 7) == 3 while steps remain undoes the
-   last crossing on the hit axis, flips that axis's step and direction, and continues. */
+/* refractRay(vec3, vec3, float, float) (:196-209) with n1 = 1.0, n2 = 1.1 and normal = the hit
+   axis times its step (:222-223); dot as ((x + y) + z), no fused operations. */
+static void o_refract_dir(float d[3], int ax, int st_ax) {
+    const float r = 1.0f / 1.1f;
+    float n[3] = {0.0f, 0.0f, 0.0f};
+    n[ax] = (float)st_ax;
+    float c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
+    if (c1 < 0.0f) {
+        for (int a = 0; a < 3; a++) n[a] = -n[a];
+        c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
+    }
+    const float c2 = sqrtf(1.0f - r * r * (1.0f - c1 * c1));
+    const float k = r * c1 - c2;
+    for (int a = 0; a < 3; a++) d[a] = r * d[a] + k * n[a];
+}
+
+/* o_cast with reflections and refractions.  A hit on a block with (flags & 7) == 3 while steps
+   remain undoes the last crossing on the hit axis, flips that axis's step and direction, and
+   continues (reflectRay :170-189).  A hit on a non-liquid block with (flags & 7) == 5 (liquid is
+   empty in castRayFromCam) while steps remain tints by 0.95 and continues; the first one also
+   bends the ray (refractRay :211-240): the origin-based exact position (never advanced by the DDA,
+   as in the shader) gets +1 on the other axes with a negative step, the direction is refracted, the
+   ray rebuilt (A1), exact += min(step, 0) and deltaPos = absDelta - (exact - round) * delta from
+   the current cell.  *mod = finalColorMod (0.94 per reflection, 0.95 per refractive block, in
+   order). */
 static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3], const float dir_in[3], int steps, orayres* R,
-                        float dir[3], int* nrefl) {
+                        float dir[3], int* nrefl, float* mod) {
     int st[3];
     double dl[3], ad[3], ex[3], dp[3];
     int r[3], last[3];
+    int bent = 0;
     for (int a = 0; a < 3; a++) {
         dir[a] = dir_in[a];
         st[a] = dir[a] < 0 ? -1 : 1;
@@ -1227,6 +1251,7 @@ static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3],
     memset(R, 0, sizeof(*R));
     R->axis = -1;
     *nrefl = 0;
+    *mod = 1.0f;
     for (int a = 0; a < 3; a++) last[a] = r[a];
     while (steps--) {
         int ax;
@@ -1251,6 +1276,24 @@ static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3],
                 st[ax] = -st[ax];
                 dir[ax] = -dir[ax];
                 (*nrefl)++;
+                *mod *= 0.94f;
+                continue;
+            }
+            if ((f & 7u) == 5u && steps > 0) {
+                *mod *= 0.95f;
+                if (!bent) {
+                    bent = 1;
+                    for (int a = 0; a < 3; a++)
+                        if (a != ax && st[a] < 0) ex[a] += 1;
+                    o_refract_dir(dir, ax, st[ax]);
+                    for (int a = 0; a < 3; a++) {
+                        st[a] = dir[a] < 0 ? -1 : 1;
+                        dl[a] = (double)(1.0f / dir[a]);
+                        ad[a] = o_gabs(dl[a]);
+                        if (st[a] < 0) ex[a] -= 1;
+                    }
+                    for (int a = 0; a < 3; a++) dp[a] = ad[a] - (ex[a] - (double)r[a]) * dl[a];
+                }
                 continue;
             }
             memcpy(R->pos, r, sizeof(r));
@@ -1301,9 +1344,8 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
     orayres R;
     float dir[3];
     int nrefl;
-    o_cast_refl(gb, world, org, d0, steps, &R, dir, &nrefl);
-    float m = 1.0f;
-    for (int i = 0; i < nrefl; i++) m *= 0.94f;
+    float m;
+    o_cast_refl(gb, world, org, d0, steps, &R, dir, &nrefl, &m);
     float c[3];
     if (look && R.pos[0] == look[0] && R.pos[1] == look[1] && R.pos[2] == look[2]) {
         float b[3];

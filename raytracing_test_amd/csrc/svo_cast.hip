@@ -493,11 +493,34 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
 #endif
 }
 
-// Reflections of the shading pass (reflectRay, low_res.frag:170-189): direction after them and count.
+// Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
+// direction after them, reflection count, finalColorMod, and whether the ray was bent.
 struct Bounce {
     float d[3];
     int32_t n;
+    float m;
+    bool bent;
 };
+
+// refractRay(vec3, vec3, float, float) (low_res.frag:196-209), n1 = 1.0, n2 = 1.1, normal = the hit
+// axis times its step (:222-223); dot as ((x + y) + z), no fused operations (-ffp-contract=off)
+__device__ __forceinline__ void refract_dir(float d[3], uint32_t ax, int32_t st_ax) {
+    const float r = 1.0f / 1.1f;
+    float n[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        if (ax == (uint32_t)k) n[k] = (float)st_ax;
+    float c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
+    if (c1 < 0.0f) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) n[k] = -n[k];
+        c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
+    }
+    const float c2 = svo::sqrt_rn(1.0f - r * r * (1.0f - c1 * c1));
+    const float kf = r * c1 - c2;
+#pragma unroll
+    for (int k = 0; k < 3; k++) d[k] = r * d[k] + kf * n[k];
+}
 
 template <bool STATS, bool REFLECT = false>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
@@ -523,8 +546,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     R.axis = 3u;
     R.tlast = 0.0f;
     // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_lt_w)
-    const bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
-                      exact_axis(R.T[2], R.a(2), budget);
+    bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
+                exact_axis(R.T[2], R.a(2), budget);
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -636,7 +659,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             }
 #endif
         }
-        if (REFLECT && hit && R.steps > 0 && (P.mat_flags[mat] & 7u) == 3u) {
+        const uint32_t mflags = REFLECT && hit ? (P.mat_flags[mat] & 7u) : 0u;
+        if (REFLECT && R.steps > 0 && mflags == 3u) {
             // a reflective block (flags & 7 == 3) with budget left: undo the last crossing on the
             // hit axis, mirror that axis (step and direction) and take the next DDA step from the
             // block, as low_res.frag:170-189 + :319-331 do
@@ -650,6 +674,50 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 }
             }
             bounce->n++;
+            bounce->m *= 0.94f;
+            dda_step(R);
+            hit = false;
+            done = false;
+            mat = 0u;
+        } else if (REFLECT && R.steps > 0 && mflags == 5u) {
+            // a refractive solid (liquid is empty here, as in castRayFromCam) with budget left:
+            // tint by 0.95 and pass; the first one bends the ray (refractRay, :211-240).  The
+            // shader's exact position is never advanced by its DDA: it is the origin (minus 1 on
+            // axes with a negative initial step), +1 on the other axes with a negative step, then
+            // min(new step, 0); deltaPos restarts from the current cell.
+            bounce->m *= 0.95f;
+            if (!bounce->bent) {
+                bounce->bent = true;
+                const uint32_t ax = R.axis;
+                int32_t sa = 1;
+#pragma unroll
+                for (int k = 0; k < 3; k++)
+                    if (ax == (uint32_t)k) sa = R.s[k];
+                refract_dir(bounce->d, ax, sa);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    double ex = (double)o[k];
+                    if (d[k] < 0.0f) ex -= 1.0;
+                    if (ax != (uint32_t)k && R.s[k] < 0) ex += 1.0;
+                    const float dk = bounce->d[k];
+                    const int32_t s = dk < 0.0f ? -1 : 1;
+                    const double delta = (double)svo::div_rn(1.0f, dk);
+                    const double ad = delta >= 0.0 ? delta : -delta;
+                    if (s < 0) ex -= 1.0;
+                    R.T[k] = ad - (ex - (double)R.r[k]) * delta;
+                    R.s[k] = s;
+#if SVO_A_F64
+                    R.ad[k] = ad;
+#else
+                    R.af[k] = (float)ad;
+#endif
+#if SVO_INV_A
+                    R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
+#endif
+                }
+                fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && exact_axis(R.T[0], R.a(0), R.steps) &&
+                       exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
+            }
             dda_step(R);
             hit = false;
             done = false;
@@ -697,7 +765,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 // ------------------------------------------------------------------------------------------------
 // Shading: low_res.frag's colour model over castRayFromCam hits — sky
 // (genSkyBox :157-168), sun lighting (calcLightIntensity :242-252), 75-step shadow ray (:373-391),
-// the looked-at block highlight (:340-343) and reflections (:170-189, applied inside trace).
+// the looked-at block highlight (:340-343), reflections (:170-189) and refractions of solids
+// (:196-240); the last two are applied inside trace.
 // Single precision in the shader's operation order (-ffp-contract=off).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float3 color_of(uint64_t c) {  // color_int_to_vec3 (:139-145)
@@ -797,7 +866,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         out = 0;
     }
     if (SHADE && out >= 0) {
-        Bounce bn = {{d[0], d[1], d[2]}, 0};
+        Bounce bn = {{d[0], d[1], d[2]}, 0, 1.0f, false};
         const Hit h = trace<false, true>(P, rsrc, path, o, d, P.steps, nullptr, &bn);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
@@ -805,8 +874,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
             P.info[out] = h.info;
         }
         const bool hit = (h.info & HIT_BIT) != 0u;
-        float m = 1.0f;  // finalColorMod
-        for (int32_t i = 0; i < bn.n; i++) m *= 0.94f;
+        const float m = bn.m;  // finalColorMod
         float3 c;
         if (P.look_valid && h.x == P.look[0] && h.y == P.look[1] && h.z == P.look[2]) {
             const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);

@@ -105,3 +105,55 @@ def test_shade_depth12_sampled(rt, oracle_mod, torch_cuda):
     # hit records are indexed by pixel row from the bottom: the frame is unsharded, index = py * W + px
     g = rt.decode_hits(hits)
     _check(rgba[torch_cuda.as_tensor(pix, device=rgba.device)], ref, g["hit"][pix], "depth12")
+
+
+GLASS, MIRROR = 0x4, 0x2
+
+
+def _glass_edits():
+    """glass (flags 4 -> stored 5) in view of both cameras, a mirror behind a glass wall, a 4^3 glass block"""
+    pts, flags = [], []
+    for x in (60, 61):  # wall across camera 0's view
+        for y in range(44, 57):
+            for z in range(40, 91):
+                pts.append((x, y, z)); flags.append(GLASS)
+    for y in range(44, 57):  # mirror behind it
+        for z in range(50, 71):
+            pts.append((70, y, z)); flags.append(MIRROR)
+    for x in range(30, 101):  # slab in camera 1's view, above the terrain
+        for z in range(30, 101):
+            for y in (62, 63):
+                pts.append((x, y, z)); flags.append(GLASS)
+    return np.array(pts, np.int32), np.array(flags, np.uint32)
+
+
+@pytest.fixture(scope="module")
+def glass_worlds(rt, oracle_mod, torch_cuda):
+    pts, flags = _glass_edits()
+    colors = (np.arange(len(pts), dtype=np.uint64) * np.uint64(2654435761)) % np.uint64(1 << 63)
+    w = rt.World.reference()
+    w.put_blocks(pts, flags, colors)
+    w.put_block(100, 72, 100, GLASS, 777, level=w.levels)  # a 4^3 glass block (one uniform node)
+    o = oracle_mod.Tree.reference_world()
+    for p, f, c in zip(pts, flags, colors):
+        o.put_block(int(p[0]), int(p[1]), int(p[2]), int(f), int(c))
+    o.put_block(100, 72, 100, GLASS, 777, level=5)
+    return w.build().upload(0), o
+
+
+@pytest.mark.parametrize("cam", [0, 1])
+def test_shade_refraction(rt, glass_worlds, cam):
+    """refractive solids (flags & 7 == 5): tint 0.95 per block passed, the first one bends the ray"""
+    gt, ot = glass_worlds
+    org, cd = CAMERAS[cam]
+    cam_dir = rt.normalize(cd)
+    for S in (300, 40):
+        rgba, hits = gt.shade_frame(org, cam_dir, 240, 136, S, sun=rt.sun_dir(), with_hits=True)
+        ref = ot.shade_frame(org, cam_dir, 240, 136, S, rt.sun_dir())
+        _check(rgba, ref, rt.decode_hits(hits)["hit"], "glass cam%d S=%d" % (cam, S))
+        if S != 300:
+            continue
+        # the bend is exercised: the shading pass ends elsewhere than the plain cast on many rays
+        plain = rt.decode_hits(gt.cast_frame(org, cam_dir, 240, 136, S))["pos"]
+        moved = np.any(rt.decode_hits(hits)["pos"] != plain, axis=1).sum()
+        assert moved > 500, moved
