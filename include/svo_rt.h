@@ -202,6 +202,9 @@ typedef struct {
 #define SVO_CAST_TIMELINE 32
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
 #define SVO_CAST_XCD_SWIZZLE 16
+/* svo_cast_desc.flags, AO (results identical): trace every AO ray through the tree instead of the
+   per-face voxel plan (A/B reference path) */
+#define SVO_CAST_AO_TRACE 128
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

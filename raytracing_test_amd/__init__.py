@@ -36,6 +36,7 @@ CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.s
 CAST_BOTTOM_FIRST = 4  # scheduling: bottom tile rows first (default is top first)
 CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
 CAST_TIMELINE = 32  # per-block start/end stamps only
+CAST_AO_TRACE = 128  # AO: trace every AO ray instead of the per-face voxel plan (A/B reference)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",

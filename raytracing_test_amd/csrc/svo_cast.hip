@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/svo_rt.h"
 #include "svo_hip.h"
@@ -51,6 +53,7 @@ struct CastParams {
     // hemisphere AO (A8)
     int32_t ao_n, ao_steps;
     float ao_tab[3 * 64];
+    const uint32_t* ao_plan;  // device AO plan (ao_plan_build) or null
     // shading: palette colours / flags, sun, highlighted block, shadow budget
     const uint64_t* mat_color;
     const uint32_t* mat_flags;
@@ -522,10 +525,12 @@ __device__ __forceinline__ void refract_dir(float d[3], uint32_t ax, int32_t st_
     for (int k = 0; k < 3; k++) d[k] = r * d[k] + kf * n[k];
 }
 
+// par_out: receives the parent of the region the ray ended in (it holds the final voxel; the LDS
+// path holds its ancestors at depths 0 .. levels-1-sh/2)
 template <bool STATS, bool REFLECT = false>
 __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
-                                     Bounce* bounce = nullptr) {
+                                     Bounce* bounce = nullptr, Parent* par_out = nullptr) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -724,6 +729,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             mat = 0u;
         }
     }
+    if (par_out) *par_out = par;
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
         const uint32_t work = st.lookups + st.brick_steps + st.plain_steps;
@@ -787,6 +793,72 @@ __device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]
     const float sv = sigmoidf(1.5f - b, 1.0f, 1.6f);
     const float h3 = fminf(fmaxf(haze, 0.0f), 1.0f) * 3.0f;
     return make_float3((0.2f + h3) * modifier + sv, (0.4f + h3) * modifier + sv, (1.0f + h3) * modifier + 0.0f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Hemisphere AO from a plan (A8).  An AO ray starts at the centre of lastPos: for a cell c >= 0,
+// dda_axis gives deltaPos = absDelta - (+-0.5) * delta whatever c is, so the voxels a ray of
+// direction d visits are lastPos + a fixed offset sequence, and the ray hits iff one of its
+// ao_steps voxels is solid (castRayFromCam never tests the start voxel).  The host simulates the
+// DDA of every (sample, hit face) once (ao_plan_build); per face the plan lists the distinct
+// offsets, each with the mask of samples passing through it.  Per hit, each offset is tested once
+// (skipped when all its samples already hit) with a read-only lookup that starts at the deepest
+// node of the primary ray's LDS path holding both the hit voxel and the tested voxel; the count is
+// the popcount of the samples hit.
+// Plan layout (u32 words): [0..5] offsets per face (face = 2*axis + (sign < 0)), [6] stride,
+// [7] 0, then per face `stride` entries of 4 words: packed offset (dx+128 | dy+128 << 8 |
+// dz+128 << 16), 0, sample mask (lo, hi).
+// ------------------------------------------------------------------------------------------------
+// solid mask of the 4^3 brick holding voxel w (an empty or SOLID region of any level covers whole
+// bricks: 0 or ~0)
+__device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const uint32_t w[3],
+                                               const uint32_t hw[3], int32_t dmax) {
+    const uint32_t diff = ((w[0] ^ hw[0]) | (w[1] ^ hw[1]) | (w[2] ^ hw[2])) | 1u;
+    const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1), dmax);
+    uint64_t mask = path.mask[da * kBlock];
+    uint32_t ref = path.ref[da * kBlock];
+    uint32_t sh = (uint32_t)(2 * (P.levels - 1 - da));
+    uint64_t res = 0ull;
+    bool more = true;
+    while (more) {
+        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
+        more = false;
+        if ((mask >> sl) & 1ull) {
+            const Node n = load_node(rsrc, ref + (uint32_t)__popcll(mask & ((1ull << sl) - 1ull)));
+            const uint32_t kind = n.info & K_KIND_MASK;
+            if (kind == K_INTERIOR) {
+                mask = n.mask;
+                ref = n.ref;
+                sh -= 2u;
+                more = true;
+            } else {
+                res = kind == K_SOLID ? ~0ull : n.mask;
+            }
+        }
+    }
+    return res;
+}
+
+__device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
+                                                  const Parent& pfin, const Hit& h, const int32_t l[3], uint32_t ax, int32_t sg) {
+    const uint32_t face = 2u * ax + (sg < 0 ? 1u : 0u);
+    const uint32_t nd = P.ao_plan[face], stride = P.ao_plan[6];
+    const uint4* ent = reinterpret_cast<const uint4*>(P.ao_plan + 8) + face * stride;
+    const uint32_t wm = P.wmask;
+    const uint32_t hw[3] = {(uint32_t)h.x & wm, (uint32_t)h.y & wm, (uint32_t)h.z & wm};
+    const int32_t dmax = P.levels - 1 - (int32_t)(pfin.sh >> 1);
+    const uint64_t all = P.ao_n >= 64 ? ~0ull : ((1ull << P.ao_n) - 1ull);
+    uint64_t hits = 0ull;
+    for (uint32_t j = 0; j < nd && hits != all; j++) {
+        const uint4 e = ent[j];
+        const uint64_t sm = (uint64_t)e.z | ((uint64_t)e.w << 32);
+        if ((hits & sm) == sm) continue;  // every sample through this voxel already hit
+        const uint32_t w[3] = {(uint32_t)(l[0] + (int32_t)(e.x & 255u) - 128) & wm, (uint32_t)(l[1] + (int32_t)((e.x >> 8) & 255u) - 128) & wm,
+                               (uint32_t)(l[2] + (int32_t)((e.x >> 16) & 255u) - 128) & wm};
+        // (a one-brick cache of the last lookup measured 2 % slower)
+        if ((brick_near(P, rsrc, path, w, hw, dmax) >> child_slot(w[0], w[1], w[2], 0u)) & 1ull) hits |= sm;
+    }
+    return (uint32_t)__popcll(hits);
 }
 
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
@@ -905,7 +977,9 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         }
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
-        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr);
+        Parent pfin;
+        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+                                   nullptr, AO ? &pfin : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -916,6 +990,10 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                 const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
                 const int32_t st = (h.info & NEG_BIT) ? -1 : 1;  // step on the hit axis
                 const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
+                const int32_t l[3] = {lx, ly, lz};
+                if (P.ao_plan && pfin.valid && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
+                    cnt = ao_count_plan(P, rsrc, path, pfin, h, l, ax, -st);
+                } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
                 for (int32_t i = 0; i < P.ao_n; i++) {
                     const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
@@ -923,6 +1001,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                     ao_dir(hv, ax, -st, ad);
                     const Hit a = trace<false>(P, rsrc, path, ao_o, ad, P.ao_steps);
                     cnt += (a.info & HIT_BIT) ? 1u : 0u;
+                }
                 }
             }
             P.ao[out] = (uint8_t)cnt;
@@ -936,6 +1015,75 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
             P.stats[SVO_STATS_HEADER + 2 * blockIdx.x + 1] = t_end;
         }
     }
+}
+
+// The AO plan of (n samples, `steps`) (see ao_count_plan): every (sample, face) ray simulated with
+// the kernel's DDA from the centre of cell 0 — dda_axis, then dda_step's axis rule in double.
+// Offsets are listed by step index, then sample, first appearance only.  Cached on the tree.
+static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float* tab, const uint32_t** out) {
+    *out = nullptr;
+    if (steps > 127 || n > 64) return SVO_OK;  // offsets are packed in bytes, masks in 64 bits: rays
+    if (t->d_ao_plan && t->ao_plan_n == n && t->ao_plan_steps == steps) {
+        *out = reinterpret_cast<const uint32_t*>(t->d_ao_plan);
+        return SVO_OK;
+    }
+    std::vector<std::vector<std::pair<uint32_t, uint64_t>>> faces(6);
+    for (int face = 0; face < 6; face++) {
+        const uint32_t ax = (uint32_t)face >> 1;
+        const int32_t sg = (face & 1) ? -1 : 1;
+        std::vector<std::vector<uint32_t>> seq(n);
+        for (int32_t i = 0; i < n; i++) {
+            float dir[3];
+            ao_dir(tab + 3 * i, ax, sg, dir);
+            double T[3], A[3];
+            int32_t st[3], pos[3] = {0, 0, 0};
+            for (int k = 0; k < 3; k++) {
+                const Dda1 a = dda_axis(0.5f, dir[k]);
+                T[k] = a.dpos;
+                A[k] = (double)(float)a.adelta;
+                st[k] = a.step;
+            }
+            for (int32_t j = 0; j < steps; j++) {
+                const bool cx = (T[0] < T[1]) && (T[0] < T[2]);
+                const bool cy = !cx && (T[1] < T[2]);
+                const int k = cx ? 0 : (cy ? 1 : 2);
+                pos[k] += st[k];
+                T[k] = T[k] + A[k];
+                seq[i].push_back((uint32_t)(pos[0] + 128) | ((uint32_t)(pos[1] + 128) << 8) | ((uint32_t)(pos[2] + 128) << 16));
+            }
+        }
+        auto& f = faces[face];
+        for (int32_t j = 0; j < steps; j++)
+            for (int32_t i = 0; i < n; i++) {
+                const uint32_t key = seq[i][j];
+                size_t e = 0;
+                while (e < f.size() && f[e].first != key) e++;
+                if (e == f.size()) f.push_back({key, 0ull});
+                f[e].second |= 1ull << i;
+            }
+    }
+    size_t stride = 1;
+    for (auto& f : faces) stride = std::max(stride, f.size());
+    std::vector<uint32_t> img(8 + 6 * stride * 4, 0u);
+    img[6] = (uint32_t)stride;
+    for (int face = 0; face < 6; face++) {
+        img[face] = (uint32_t)faces[face].size();
+        for (size_t e = 0; e < faces[face].size(); e++) {
+            uint32_t* w = &img[8 + (face * stride + e) * 4];
+            w[0] = faces[face][e].first;
+            w[2] = (uint32_t)faces[face][e].second;
+            w[3] = (uint32_t)(faces[face][e].second >> 32);
+        }
+    }
+    if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
+    t->d_ao_plan = nullptr;
+    t->ao_plan_steps = -1;
+    HIP_TRY(hipMalloc(&t->d_ao_plan, img.size() * sizeof(uint32_t)), SVO_ENOMEM);
+    HIP_TRY(hipMemcpy(t->d_ao_plan, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    t->ao_plan_n = n;
+    t->ao_plan_steps = steps;
+    *out = reinterpret_cast<const uint32_t*>(t->d_ao_plan);
+    return SVO_OK;
 }
 
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
@@ -958,7 +1106,13 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.ao = o->ao;
     P.ao_n = d->ao_samples;
     P.ao_steps = d->ao_steps;
-    if (P.ao_n > 0) hemisphere_table(P.ao_n, P.ao_tab);
+    if (P.ao_n > 0) {
+        hemisphere_table(P.ao_n, P.ao_tab);
+        if (!(P.flags & SVO_CAST_AO_TRACE)) {
+            int rc = ao_plan_get(t, P.ao_n, P.ao_steps, P.ao_tab, &P.ao_plan);
+            if (rc) return rc;
+        }
+    }
     if (d->ray_dirs) {
         P.mode = MODE_EXPLICIT;
         P.rdir = d->ray_dirs;
@@ -996,6 +1150,9 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_mats) (void)hipFree(t->d_mats);
     if (t->d_pal) (void)hipFree(t->d_pal);
     if (t->d_work) (void)hipFree(t->d_work);
+    if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
+    t->d_ao_plan = nullptr;
+    t->ao_plan_steps = -1;
     (void)hipSetDevice(prev);
     t->d_nodes = t->d_mats = t->d_work = t->d_pal = nullptr;
     t->dev_node_cap = t->dev_mat_cap = t->dev_pal_n = 0;

@@ -48,6 +48,9 @@ struct svo_tree {
     void* d_mats = nullptr;
     void* d_work = nullptr;   // scheduler counters (ring)
     void* d_pal = nullptr;    // palette for shading: u64 colour[n] then u32 flags[n]
+    // hemisphere AO plan (svo_cast.hip, built on first use for (ao_samples, ao_steps))
+    mutable void* d_ao_plan = nullptr;
+    mutable int32_t ao_plan_n = 0, ao_plan_steps = -1;
     uint32_t work_slots = 0;
     uint32_t work_next = 0;
     uint64_t device_bytes = 0;

@@ -273,14 +273,29 @@ def test_depth12_full_frame_properties(rt, depth12):
 
 @pytest.mark.parametrize("n_ao", [16, 20])
 def test_ao_reference_world(rt, gtree, ref_world_oracle, n_ao):
-    """A8 / C4: hemisphere AO counts (per pixel, rays that hit within 5 steps) against the oracle."""
+    """A8 / C4: hemisphere AO counts (per pixel, rays that hit within 5 steps) against the oracle,
+    through the per-face voxel plan (default) and by tracing every AO ray (CAST_AO_TRACE)."""
     for org, d in CAMERAS[:3]:
         dn = rt.normalize(d)
-        out = rt.decode_hits(gtree.cast_frame(org, dn, 128, 128, 300, ao_samples=n_ao, ao_steps=5))
         ao, hit = ref_world_oracle.cast_frame_ao(org, dn, 128, 128, 300, n_ao, 5)
+        for flags in (0, rt.CAST_AO_TRACE):
+            out = rt.decode_hits(gtree.cast_frame(org, dn, 128, 128, 300, ao_samples=n_ao, ao_steps=5, flags=flags))
+            assert np.array_equal(out["hit"], hit != 0)
+            assert np.array_equal(out["ao"], ao), (org, n_ao, flags)
+            assert out["ao"].max() <= n_ao
+
+
+@pytest.mark.parametrize("n_ao,ao_steps", [(1, 5), (16, 0), (16, 1), (20, 12), (64, 3), (7, 40)])
+def test_ao_plan_budgets(rt, gtree, ref_world_oracle, n_ao, ao_steps):
+    """The AO plan over sample counts and budgets (1 .. 64 samples, 0 .. 40 steps) against the oracle."""
+    # the C1 pose, and one whose hits lie at negative (wrapped) coordinates: those AO rays do not
+    # start at lastPos (trunc of -x.5) and are traced instead of planned
+    for org, d in (CAMERAS[1], ((-30.5, 60.0, -10.5), (-1.0, -0.6, -0.4))):
+        dn = rt.normalize(d)
+        ao, hit = ref_world_oracle.cast_frame_ao(org, dn, 96, 64, 300, n_ao, ao_steps)
+        out = rt.decode_hits(gtree.cast_frame(org, dn, 96, 64, 300, ao_samples=n_ao, ao_steps=ao_steps))
         assert np.array_equal(out["hit"], hit != 0)
-        assert np.array_equal(out["ao"], ao), (org, n_ao)
-        assert out["ao"].max() <= n_ao
+        assert np.array_equal(out["ao"], ao), (org, n_ao, ao_steps)
 
 
 def test_ao_depth12_sampled(rt, oracle_mod, depth12):
@@ -290,6 +305,8 @@ def test_ao_depth12_sampled(rt, oracle_mod, depth12):
     pix = np.random.default_rng(2).integers(0, 1920 * 1080, 3000)
     ao, hit = T.cast_frame_ao((4, 90, 4), dn, 1920, 1080, 16384, 16, 5, pixels=pix, nthreads=16)
     assert np.array_equal(out["ao"][pix], ao)
+    tr = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=16, ao_steps=5, flags=rt.CAST_AO_TRACE))
+    assert np.array_equal(out["ao"], tr["ao"])  # plan == traced AO rays over the whole frame
     assert out["ao"].mean() > 0.5  # terrain occludes part of the hemisphere
 
 
