@@ -14,7 +14,8 @@ reported time is the max over ranks.
 Extra objects on the JSON line:
   roofline     — the cast kernel's algorithmic bytes (B_ray = 16*E_node +
                  4*E_child + B_out per ray, E from profiles/bray.json) / its average launch time,
-                 measured with HIP events on the launch stream, against the 8 TB/s HBM peak;
+                 measured with HIP events on the launch stream (N=1: one pair around the timed
+                 region, gaps between launches included), against the 8 TB/s HBM peak;
                  traffic = HBM bytes per launch from the committed rocprofv3 PMC pass (or null).
   cpu_baseline — the oracle's C restatement of castRayFromCam + getBlock (reference layout, full
                  descent per step) timed on this host's cores on the same frame (rank 0, N=1).
@@ -115,6 +116,9 @@ def main():
                     help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray), "
                          "rgba gathered instead of hit records")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--launch-events", action="store_true",
+                    help="an event pair around every cast launch (default at N=1: one pair around the timed region, whose "
+                         "average per launch includes the gaps between launches; per-launch pairs cost ~7 us per step)")
     args = ap.parse_args()
 
     import torch
@@ -199,15 +203,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nframes)] for _ in range(args.steps)]
+    reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    # at N=1 the launches run back to back on one stream: one event pair around the timed region
+    # gives their average (gaps included); with a gather in between, pairs around each launch
+    args.region_events = world == 1 and not args.launch_events
     t0 = time.perf_counter()
+    if args.region_events:
+        reg[0].record(stream)
     for k in range(args.steps):
-        one_step(evs[k])
+        one_step(None if args.region_events else evs[k])
+    if args.region_events:
+        reg[1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = [e[0].elapsed_time(e[1]) for step in evs for e in step]
+    if args.region_events:  # launches back to back on one stream (no gather in between at N=1)
+        kern_ms = [reg[0].elapsed_time(reg[1]) / (args.steps * nframes)]
+    else:
+        kern_ms = [e[0].elapsed_time(e[1]) for step in evs for e in step]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -219,7 +234,7 @@ def main():
 
     if args.stats and rank == 0:
         d0 = descs[0]
-        nblk = ((W + 7) // 8) * len(range(d0.tile_row_start, (H + 7) // 8, d0.tile_row_step))  # 8x8 tiles: >= blocks
+        nblk = rt.Tree.blocks(d0)
         for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
             st = torch.zeros(rt.STATS_HEADER + 2 * nblk + W * H, dtype=torch.int64, device=dev)
             d0.flags |= mode
@@ -293,6 +308,8 @@ def main():
                    "tree_builder": "host" if args.host_build else "gpu"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
+                         "included)" if args.region_events else "a HIP event pair around every launch on its stream",
     }
     print(json.dumps(line), flush=True)
     if world > 1:

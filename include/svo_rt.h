@@ -182,8 +182,8 @@ typedef struct {
                           wave-level brick voxel steps, (reserved), lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
-                          per-lane path; then 2 stamps per block (room for one block per
-                          8x8 tile); then, with SVO_CAST_STATS in frame mode, one word per
+                          per-lane path; then 2 stamps per block (svo_cast_blocks);
+                          then, with SVO_CAST_STATS in frame mode, one word per
                           output pixel: lookups | brick steps << 32
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
 } svo_cast_desc;
@@ -197,7 +197,7 @@ typedef struct {
    (longest rays first); this bit restores bottom-first order */
 #define SVO_CAST_BOTTOM_FIRST 4
 /* svo_cast_desc.flags: write per-block start/end stamps (100 MHz) to stats[SVO_STATS_HEADER + 2*block] only;
-   stats must hold SVO_STATS_HEADER + 2 * (8x8 tiles of the launch) [+ pixels with SVO_CAST_STATS] words */
+   stats must hold SVO_STATS_HEADER + 2 * svo_cast_blocks() [+ pixels with SVO_CAST_STATS] words */
 #define SVO_STATS_HEADER 32
 #define SVO_CAST_TIMELINE 32
 /* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
@@ -205,9 +205,15 @@ typedef struct {
 /* svo_cast_desc.flags, AO (results identical): trace every AO ray through the tree instead of the
    per-face voxel plan (A/B reference path) */
 #define SVO_CAST_AO_TRACE 128
+/* svo_cast_desc.flags, scheduling (results identical): in frame mode each wavefront (one block)
+   covers 16x4 pixels of its 8-pixel tile row; these bits select 8x8 or 32x2 instead */
+#define SVO_CAST_TILE_8X8 256
+#define SVO_CAST_TILE_32X2 512
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);
+/* number of blocks (64-lane wavefronts) a cast of this desc launches */
+int svo_cast_blocks(const svo_cast_desc* d, int64_t* n);
 /* asynchronous on hip_stream */
 int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* out, void* hip_stream);
 /* RAY_CASTER::castRayFromCam with explicit camera (synchronous, one ray on the GPU) */

@@ -37,6 +37,8 @@ CAST_BOTTOM_FIRST = 4  # scheduling: bottom tile rows first (default is top firs
 CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
 CAST_TIMELINE = 32  # per-block start/end stamps only
 CAST_AO_TRACE = 128  # AO: trace every AO ray instead of the per-face voxel plan (A/B reference)
+CAST_TILE_8X8 = 256  # scheduling: one wavefront per 8x8 tile (default: 16x4 pixels of its 8-pixel tile row)
+CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel tile row
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
@@ -120,7 +122,7 @@ ABI_SYMBOLS = (
     "svo_last_error", "svo_version", "svo_world_create", "svo_world_destroy", "svo_init_tetra_hexa_tree",
     "svo_put_block", "svo_get_block", "svo_delete_block", "svo_gen_world", "svo_world_node_count", "svo_build",
     "svo_build_terrain", "svo_tree_get_info", "svo_tree_palette", "svo_tree_get_block", "svo_tree_export",
-    "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
+    "svo_upload", "svo_tree_destroy", "svo_cast_count", "svo_cast_blocks", "svo_cast_rays", "svo_cast_ray_from_cam", "svo_sync",
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
@@ -167,6 +169,7 @@ def lib():
     L.svo_tree_destroy.argtypes = [vp]
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
+    L.svo_cast_blocks.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
     L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
     L.svo_shade_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(ShadeDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_ray_from_cam.argtypes = [vp, f3, f3, i32, C.POINTER(RayResult), C.POINTER(Block)]
@@ -457,6 +460,13 @@ class Tree:
     def count(desc):
         n = C.c_int64()
         _check(lib().svo_cast_count(C.byref(desc), C.byref(n)), "svo_cast_count")
+        return n.value
+
+    @staticmethod
+    def blocks(desc):
+        """blocks (64-lane wavefronts) a cast of desc launches: the stats buffer holds 2 stamps each"""
+        n = C.c_int64()
+        _check(lib().svo_cast_blocks(C.byref(desc), C.byref(n)), "svo_cast_blocks")
         return n.value
 
     @staticmethod

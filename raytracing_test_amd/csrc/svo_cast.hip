@@ -41,6 +41,7 @@ struct CastParams {
     float org[3];
     float sdir[3];
     int32_t width, height, tiles_x, tile_row_start, tile_row_step, tile_rows_local;
+    int32_t tile_lh;  // log2 of a wavefront's pixel rows (frame_wave_lh)
     // explicit mode
     const float* rdir;
     const float* rorg;
@@ -53,7 +54,7 @@ struct CastParams {
     // hemisphere AO (A8)
     int32_t ao_n, ao_steps;
     float ao_tab[3 * 64];
-    const uint32_t* ao_plan;  // device AO plan (ao_plan_build) or null
+    const uint32_t* ao_plan;  // device AO plan (ao_plan_get) or null
     // shading: palette colours / flags, sun, highlighted block, shadow budget
     const uint64_t* mat_color;
     const uint32_t* mat_flags;
@@ -75,13 +76,16 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #define SVO_UNIFORM_DIRS 1
 #endif
 #ifndef SVO_BRICK_PACK
-#define SVO_BRICK_PACK 1
+#define SVO_BRICK_PACK 2
 #endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
 #ifndef SVO_FMA
 #define SVO_FMA 1
+#endif
+#ifndef SVO_VROOT
+#define SVO_VROOT 1  // start every ray below a virtual parent of the root (no first-lookup branch)
 #endif
 #ifndef SVO_A_F64
 #define SVO_A_F64 0  // keep absDelta in f64 registers (A/B)
@@ -176,6 +180,89 @@ __device__ __forceinline__ void dda_step(Ray& R) {
     R.steps--;
 }
 
+#ifndef SVO_BOX_V2
+#define SVO_BOX_V2 1
+#endif
+// Wave-uniform step directions per axis: 1 = every active lane steps +, 2 = every one steps -,
+// 0 = mixed.  Lanes only retire while a ray runs, so flags taken at its start stay true.
+__device__ __forceinline__ void dir_flags(const int32_t s[3], uint32_t ud[3]) {
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint64_t b = __ballot(s[k] > 0);
+        ud[k] = b == ex ? 1u : (b == 0ull ? 2u : 0u);
+    }
+}
+
+#if SVO_BOX_V2
+// A run of free cells through a 4-cell line (occupancy bits 0-3; higher bits are ignored) from the
+// ray's cell c (free itself) in its step direction: t = cells in the run (>= 1), m = their slots.
+// A sentinel bit stands for the end of the line: one ctz (up) or one clz (down) finds the run.
+__device__ __forceinline__ void run_up(uint32_t occ, uint32_t c, uint32_t& t, uint32_t& m) {
+    t = (uint32_t)__builtin_ctz((occ | 16u) >> c);
+    m = ((1u << t) - 1u) << c;
+}
+__device__ __forceinline__ void run_down(uint32_t occ, uint32_t c, uint32_t& t, uint32_t& m) {
+    // slots below c at bits 1..c, the sentinel at bit 0: the highest set bit is the run's first slot
+    const uint32_t lo = 31u - (uint32_t)__builtin_clz(__builtin_amdgcn_ubfe((occ << 1) | 1u, 0u, c + 1u));
+    t = c + 1u - lo;
+    m = ((1u << t) - 1u) << lo;
+}
+__device__ __forceinline__ void run_fwd(uint32_t occ, uint32_t c, bool pos, uint32_t ud, uint32_t& t, uint32_t& m) {
+    if (ud == 1u) {
+        run_up(occ, c, t, m);
+    } else if (ud == 2u) {
+        run_down(occ, c, t, m);
+    } else {
+        uint32_t t0, m0, t1, m1;
+        run_up(occ, c, t0, m0);
+        run_down(occ, c, t1, m1);
+        t = pos ? t0 : t1;
+        m = pos ? m0 : m1;
+    }
+}
+
+// per 16-bit half of v: 1 if it is nonzero — one packed min (clang scalarises the vector form)
+__device__ __forceinline__ uint32_t nonzero16(uint32_t v) {
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "s"(0x00010001u));
+    return r;
+}
+
+// Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
+// the run along x from the mask row, then whole rows along z, then whole planes along y), all from
+// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
+__device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, const uint32_t ud[3],
+                                          int32_t e[3]) {
+    const uint32_t cx = __builtin_amdgcn_ubfe(w[0], sh, 2u), cy = __builtin_amdgcn_ubfe(w[1], sh, 2u), cz = __builtin_amdgcn_ubfe(w[2], sh, 2u);
+    const bool px = s[0] > 0, py = s[1] > 0, pz = s[2] > 0;
+    const uint32_t lo = (uint32_t)pmask, hi = (uint32_t)(pmask >> 32);
+    uint32_t tx, xm, ty, ym, tz, zm;
+    // x run through the row (cy, cz)
+    run_fwd((uint32_t)(pmask >> (16u * cz + 4u * cy)), cx, px, ud[0], tx, xm);
+    // rows (cy, z) over the x run: bit z (bits 0, 16 -> 0, 1 of the low half, 2, 3 of the high) =
+    // the row holds a solid slot
+    const uint32_t xs = xm << (4u * cy);
+    const uint32_t xl = xs | (xs << 16);
+    const uint32_t zc = nonzero16(lo & xl) | (nonzero16(hi & xl) << 2);
+    run_fwd(zc | (zc >> 15), cz, pz, ud[2], tz, zm);
+    // planes y over the x run x z run: the z run's planes folded into one, rows restricted to the
+    // x run, then one bit per nonzero nibble (bit 4y+3), gathered by a multiply
+    const uint32_t zl = (0x0000FFFFu & (uint32_t)__builtin_amdgcn_sbfe((int)zm, 0u, 1u)) | (0xFFFF0000u & (uint32_t)__builtin_amdgcn_sbfe((int)zm, 1u, 1u));
+    const uint32_t zh = (0x0000FFFFu & (uint32_t)__builtin_amdgcn_sbfe((int)zm, 2u, 1u)) | (0xFFFF0000u & (uint32_t)__builtin_amdgcn_sbfe((int)zm, 3u, 1u));
+    const uint32_t pl = (lo & zl) | (hi & zh);
+    const uint32_t x2 = xm | (xm << 4);  // the x run in every nibble (shifts: v_mul_lo is quarter rate)
+    const uint32_t q = (pl | (pl >> 16)) & (x2 | (x2 << 8));
+    const uint32_t nb = (((q & 0x7777u) + 0x7777u) | q) & 0x8888u;
+    run_fwd(__builtin_amdgcn_ubfe(__umul24(nb, 0x249u), 12u, 4u), cy, py, ud[1], ty, ym);
+    (void)ym;
+    // steps to leave: t cells of 2^sh voxels, less the part of the current cell behind the ray
+    const uint32_t m = (1u << sh) - 1u;
+    e[0] = (int32_t)((tx << sh) - ((px ? w[0] : ~w[0]) & m));
+    e[1] = (int32_t)((ty << sh) - ((py ? w[1] : ~w[1]) & m));
+    e[2] = (int32_t)((tz << sh) - ((pz ? w[2] : ~w[2]) & m));
+}
+#else
 // Free slots of a 4-slot line (bit = occupied) beyond slot c in the step direction, before an
 // occupied slot or the end of the line.  Branch-free.
 __device__ __forceinline__ uint32_t run_up(uint32_t occ, uint32_t c) {
@@ -202,7 +289,8 @@ __device__ __forceinline__ uint32_t run_bits(uint32_t c, uint32_t n, bool pos) {
 // Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
 // the run along x from the mask row, then whole rows along z, then whole planes along y), all from
 // the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
-__device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, int32_t e[3]) {
+__device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, const uint32_t*,
+                                          int32_t e[3]) {
     const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
     const bool px = s[0] > 0, py = s[1] > 0, pz = s[2] > 0;
     const uint32_t lo = (uint32_t)pmask, hi = (uint32_t)(pmask >> 32);
@@ -234,6 +322,7 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     e[1] = (int32_t)((ny << sh) + ((py ? ~w[1] : w[1]) & m) + 1u);
     e[2] = (int32_t)((nz << sh) + ((pz ? ~w[2] : w[2]) & m) + 1u);
 }
+#endif
 
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
 // #{ j >= 0 : T + j*a < W } = c, exact under exact_axis.  The f32 estimate q ~ (W-T)/a is within
@@ -351,7 +440,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
-    if (par.valid) {
+    if (SVO_VROOT || par.valid) {
         // the previous voxel lies in the parent's region (every move starts inside it), so the
         // bits in which the last step changed the stepped coordinate tell whether the ray left it
         const uint32_t diff = moved;
@@ -373,6 +462,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
         }
         ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
+        if (STATS && SVO_VROOT && dd == 0) st.root_starts++;
     } else if (STATS) {
         st.root_starts++;
     }
@@ -386,6 +476,11 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
         }
         const Node n = load_node(rsrc, ni);
         const uint32_t kind = n.info & K_KIND_MASK;
+        // (read only for BRICK / SOLID results: written on every load, so the previous values need
+        // no copies around it)
+        bmask = n.mask;
+        bref = n.ref;
+        binfo = n.info;
         if (kind == K_INTERIOR) {
             const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
             path.mask[dd * kBlock] = n.mask;
@@ -401,9 +496,6 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             more = occ && dd < P.levels;
             sh_out = occ ? 0u : sh;  // (occupied at the last level only in a malformed tree: one voxel)
         } else {
-            bmask = n.mask;
-            bref = n.ref;
-            binfo = n.info;
             sh_out = 2u;
             res = kind == K_SOLID ? R_SOLID : R_BRICK;
             more = false;
@@ -434,7 +526,37 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 template <bool STATS, bool TLAST>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
-#if SVO_BRICK_PACK
+#if SVO_BRICK_PACK == 2
+    // voxel index + 64 (byte 0: the 64-bit shift reads its low 6 bits, and the +-1/4/16 moves of a
+    // walk stay within 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register
+    uint32_t pk = (left0 << 8) | (child_slot(w[0], w[1], w[2], 0u) + 64u);
+    const uint32_t d0 = (uint32_t)R.s[0] - 0x100u, d1 = (uint32_t)(R.s[1] * 4) - 0x10000u, d2 = (uint32_t)(R.s[2] * 16) - 0x1000000u;
+    bool go;
+    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
+        solid = (bmask >> (pk & 63u)) & 1ull;
+        go = !solid && R.steps > 0;
+        if (go) {
+            // one DDA step (ray_caster.cpp:70-80) without position updates
+            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+            const bool cy = !cx && (R.T[1] < R.T[2]);
+            const bool cz = !cx && !cy;
+            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            R.axis = cx ? 0u : (cy ? 1u : 2u);
+            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+            R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
+            R.steps--;
+            pk += cx ? d0 : (cy ? d1 : d2);
+            if (STATS) {
+                st.brick_steps++;
+                st.wv_brick += wave_lead();
+            }
+            go = ((pk - 0x01010100u) & ~pk & 0x80808000u) == 0u;  // no steps-left byte at 0: inside
+        }
+    } while (go);
+    left = pk >> 8;
+    return pk & 63u;
+#elif SVO_BRICK_PACK
     // steps left (bytes 0-2) and voxel index (byte 3) in one register: one select + add per step
     uint32_t pk = left0 | (child_slot(w[0], w[1], w[2], 0u) << 24);
     const uint32_t d0 = ((uint32_t)R.s[0] << 24) - 1u, d1 = ((uint32_t)(R.s[1] * 4) << 24) - 0x100u,
@@ -553,14 +675,25 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_lt_w)
     bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
                 exact_axis(R.T[2], R.a(2), budget);
+    uint32_t ud[3];
+    dir_flags(R.s, ud);
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
     Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
+#if SVO_VROOT
+    // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
+    // the whole world = node 0): the first lookup takes the same path as every later one
+    par.valid = true;
+    par.mask = 1ull;
+    par.ref = 0u;
+    par.sh = 2u * (uint32_t)P.levels;
+#else
     par.valid = false;
     par.mask = 0ull;
     par.ref = par.sh = 0u;
+#endif
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
@@ -589,7 +722,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             done = true;
         } else if (!(fast && [&] {
                        int32_t ex[3];
-                       box_exits(w, R.s, sh, par.mask, ex);
+                       if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
+                       box_exits(w, R.s, sh, par.mask, ud, ex);
                        return skip_box(R, ex);
                    }())) {
             if (STATS && fast) st.skip_out++;
@@ -637,9 +771,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             const int32_t nx = (int32_t)((left0 & 0xFFu) - (left & 0xFFu));
             const int32_t ny = (int32_t)(((left0 >> 8) & 0xFFu) - ((left >> 8) & 0xFFu));
             const int32_t nz = (int32_t)((left0 >> 16) - (left >> 16));
-            R.r[0] += __mul24(R.s[0], nx);
-            R.r[1] += __mul24(R.s[1], ny);
-            R.r[2] += __mul24(R.s[2], nz);
+            R.r[0] += R.s[0] > 0 ? nx : -nx;  // (s * n as a 24-bit multiply-add became v_mad_u64_u32)
+            R.r[1] += R.s[1] > 0 ? ny : -ny;
+            R.r[2] += R.s[2] > 0 ? nz : -nz;
 #else
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
@@ -800,14 +934,17 @@ __device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]
 // dda_axis gives deltaPos = absDelta - (+-0.5) * delta whatever c is, so the voxels a ray of
 // direction d visits are lastPos + a fixed offset sequence, and the ray hits iff one of its
 // ao_steps voxels is solid (castRayFromCam never tests the start voxel).  The host simulates the
-// DDA of every (sample, hit face) once (ao_plan_build); per face the plan lists the distinct
-// offsets, each with the mask of samples passing through it.  Per hit, each offset is tested once
-// (skipped when all its samples already hit) with a read-only lookup that starts at the deepest
-// node of the primary ray's LDS path holding both the hit voxel and the tested voxel; the count is
-// the popcount of the samples hit.
-// Plan layout (u32 words): [0..5] offsets per face (face = 2*axis + (sign < 0)), [6] stride,
-// [7] 0, then per face `stride` entries of 4 words: packed offset (dx+128 | dy+128 << 8 |
-// dz+128 << 16), 0, sample mask (lo, hi).
+// DDA of every (sample, hit face) once (ao_plan_get); per face the distinct offsets, each with the
+// mask of samples passing through it, are grouped by the 4^3 brick they fall in — which depends on
+// where lastPos sits in its brick, so there is one group list per (face, alignment).  Per hit,
+// each brick is looked up once (skipped when all its samples already hit), starting at the deepest
+// node of the primary ray's LDS path holding both the hit voxel and the brick; its solid plan voxels
+// add their samples.  The count is the popcount of the samples hit.
+// Plan layout (u32 words): [2g, 2g+1] = first record (16-B units), bricks, for g = face*64 + align
+// (face = 2*axis + (sign < 0), align = lastPos & 3 per axis as z<<4|y<<2|x); per brick: {packed
+// brick offset (bx+128 | by+128 << 8 | bz+128 << 16), 0, voxel mask lo, hi}, {union of its sample
+// masks lo, hi, 0, 0}, then one u64 sample mask per voxel of the voxel mask in bit order (padded
+// to 16 B).
 // ------------------------------------------------------------------------------------------------
 // solid mask of the 4^3 brick holding voxel w (an empty or SOLID region of any level covers whole
 // bricks: 0 or ~0)
@@ -842,21 +979,31 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdg
 __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
                                                   const Parent& pfin, const Hit& h, const int32_t l[3], uint32_t ax, int32_t sg) {
     const uint32_t face = 2u * ax + (sg < 0 ? 1u : 0u);
-    const uint32_t nd = P.ao_plan[face], stride = P.ao_plan[6];
-    const uint4* ent = reinterpret_cast<const uint4*>(P.ao_plan + 8) + face * stride;
+    const uint32_t al = ((uint32_t)l[0] & 3u) | (((uint32_t)l[1] & 3u) << 2) | (((uint32_t)l[2] & 3u) << 4);
+    const uint2 hd = reinterpret_cast<const uint2*>(P.ao_plan)[face * 64u + al];
+    const uint4* r = reinterpret_cast<const uint4*>(P.ao_plan) + hd.x;
     const uint32_t wm = P.wmask;
     const uint32_t hw[3] = {(uint32_t)h.x & wm, (uint32_t)h.y & wm, (uint32_t)h.z & wm};
+    const uint32_t hb[3] = {(uint32_t)l[0] >> 2, (uint32_t)l[1] >> 2, (uint32_t)l[2] >> 2};
     const int32_t dmax = P.levels - 1 - (int32_t)(pfin.sh >> 1);
     const uint64_t all = P.ao_n >= 64 ? ~0ull : ((1ull << P.ao_n) - 1ull);
     uint64_t hits = 0ull;
-    for (uint32_t j = 0; j < nd && hits != all; j++) {
-        const uint4 e = ent[j];
-        const uint64_t sm = (uint64_t)e.z | ((uint64_t)e.w << 32);
-        if ((hits & sm) == sm) continue;  // every sample through this voxel already hit
-        const uint32_t w[3] = {(uint32_t)(l[0] + (int32_t)(e.x & 255u) - 128) & wm, (uint32_t)(l[1] + (int32_t)((e.x >> 8) & 255u) - 128) & wm,
-                               (uint32_t)(l[2] + (int32_t)((e.x >> 16) & 255u) - 128) & wm};
-        // (a one-brick cache of the last lookup measured 2 % slower)
-        if ((brick_near(P, rsrc, path, w, hw, dmax) >> child_slot(w[0], w[1], w[2], 0u)) & 1ull) hits |= sm;
+    for (uint32_t j = 0; j < hd.y && hits != all; j++) {
+        const uint4 e = r[0], u = r[1];
+        const uint64_t vm = (uint64_t)e.z | ((uint64_t)e.w << 32), um = (uint64_t)u.x | ((uint64_t)u.y << 32);
+        const uint2* sm = reinterpret_cast<const uint2*>(r + 2);
+        r += 2u + (((uint32_t)__popcll(vm) + 1u) >> 1);
+        if ((hits & um) == um) continue;  // every sample through this brick already hit
+        // the brick's corner voxel (wrapped); its solid mask from one lookup
+        const uint32_t w[3] = {((hb[0] + (e.x & 255u) - 128u) << 2) & wm, ((hb[1] + ((e.x >> 8) & 255u) - 128u) << 2) & wm,
+                               ((hb[2] + ((e.x >> 16) & 255u) - 128u) << 2) & wm};
+        uint64_t m = brick_near(P, rsrc, path, w, hw, dmax) & vm;
+        while (m) {  // the plan voxels of this brick that are solid: their samples hit
+            const uint32_t v = (uint32_t)__builtin_ctzll(m);
+            const uint2 smv = sm[__popcll(vm & ((1ull << v) - 1ull))];
+            hits |= (uint64_t)smv.x | ((uint64_t)smv.y << 32);
+            m &= m - 1ull;
+        }
     }
     return (uint32_t)__popcll(hits);
 }
@@ -906,13 +1053,17 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
-        const int32_t px = tx * 8 + (lane & 7), py = tr * 8 + (lane >> 3);
+        // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
+        // sub-rows of one column of footprints are adjacent waves
+        const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
+        const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
+        const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
         if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
             o[0] = P.org[0];
             o[1] = P.org[1];
             o[2] = P.org[2];
-            out = ((int64_t)trl * 8 + (lane >> 3)) * P.width + px;
+            out = ((int64_t)trl * 8 + rr) * P.width + px;
         }
     } else if (P.mode == MODE_EXPLICIT) {
         if (g < P.n_rays) {
@@ -991,7 +1142,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                 const int32_t st = (h.info & NEG_BIT) ? -1 : 1;  // step on the hit axis
                 const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
                 const int32_t l[3] = {lx, ly, lz};
-                if (P.ao_plan && pfin.valid && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
+                if (P.ao_plan && pfin.valid && pfin.sh < 2u * (uint32_t)P.levels && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
                     cnt = ao_count_plan(P, rsrc, path, pfin, h, l, ax, -st);
                 } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
@@ -1062,19 +1213,46 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
                 f[e].second |= 1ull << i;
             }
     }
-    size_t stride = 1;
-    for (auto& f : faces) stride = std::max(stride, f.size());
-    std::vector<uint32_t> img(8 + 6 * stride * 4, 0u);
-    img[6] = (uint32_t)stride;
-    for (int face = 0; face < 6; face++) {
-        img[face] = (uint32_t)faces[face].size();
-        for (size_t e = 0; e < faces[face].size(); e++) {
-            uint32_t* w = &img[8 + (face * stride + e) * 4];
-            w[0] = faces[face][e].first;
-            w[2] = (uint32_t)faces[face][e].second;
-            w[3] = (uint32_t)(faces[face][e].second >> 32);
+    struct Brick {
+        uint32_t key;
+        uint64_t vm, um, sm[64];
+    };
+    std::vector<uint32_t> img(2 * 6 * 64, 0u);
+    for (int face = 0; face < 6; face++)
+        for (int al = 0; al < 64; al++) {
+            const int32_t a[3] = {al & 3, (al >> 2) & 3, al >> 4};
+            std::vector<Brick> bricks;  // in order of first use
+            for (const auto& f : faces[face]) {
+                uint32_t key = 0u, v = 0u;
+                for (int k = 0; k < 3; k++) {
+                    const int32_t p = a[k] + (int32_t)((f.first >> (8 * k)) & 255u) - 128;  // from lastPos's brick corner
+                    key |= (uint32_t)((p >> 2) + 128) << (8 * k);                            // floor division
+                    v |= (uint32_t)(p & 3) << (2 * k);
+                }
+                size_t b = 0;
+                while (b < bricks.size() && bricks[b].key != key) b++;
+                if (b == bricks.size()) {
+                    bricks.push_back(Brick{});
+                    bricks.back().key = key;
+                }
+                bricks[b].vm |= 1ull << v;
+                bricks[b].um |= f.second;
+                bricks[b].sm[v] |= f.second;
+            }
+            const size_t g = (size_t)face * 64 + (size_t)al;
+            img[2 * g] = (uint32_t)(img.size() / 4);
+            img[2 * g + 1] = (uint32_t)bricks.size();
+            for (const Brick& b : bricks) {
+                const uint32_t rec[8] = {b.key, 0u, (uint32_t)b.vm, (uint32_t)(b.vm >> 32), (uint32_t)b.um, (uint32_t)(b.um >> 32), 0u, 0u};
+                img.insert(img.end(), rec, rec + 8);
+                for (int v = 0; v < 64; v++)
+                    if ((b.vm >> v) & 1ull) {
+                        img.push_back((uint32_t)b.sm[v]);
+                        img.push_back((uint32_t)(b.sm[v] >> 32));
+                    }
+                while (img.size() % 4) img.push_back(0u);
+            }
         }
-    }
     if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
     t->d_ao_plan = nullptr;
     t->ao_plan_steps = -1;
@@ -1125,7 +1303,9 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     raygen_init(P.rg, d->cam_dir, d->ppx, d->ppy, d->width, d->height);
     P.width = d->width;
     P.height = d->height;
-    P.tiles_x = (d->width + 7) / 8;
+    // wavefronts per tile row: one per 16x4 footprint (or 8x8 / 32x2: svo_rt.h)
+    P.tile_lh = frame_wave_lh(d->flags);
+    P.tiles_x = frame_wave_cols(d->width, P.tile_lh);
     P.tile_row_start = d->tile_row_start;
     P.tile_row_step = d->tile_row_step;
     const int32_t tile_rows = (d->height + 7) / 8;

@@ -44,8 +44,19 @@ SVO_HD uint32_t node_material(uint32_t info) { return info >> 16; }
 
 // child slot of wrapped voxel coordinates at bit offset `sh` (tetrahexa_tree.cpp:127-129)
 SVO_HD uint32_t child_slot(uint32_t x, uint32_t y, uint32_t z, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // three bit-field extracts and two shift-ors (the generic form compiles to eight VALU ops)
+    return __builtin_amdgcn_ubfe(x, sh, 2u) | (__builtin_amdgcn_ubfe(y, sh, 2u) << 2) | (__builtin_amdgcn_ubfe(z, sh, 2u) << 4);
+#else
     return (((z >> sh) & 3u) << 4) | (((y >> sh) & 3u) << 2) | ((x >> sh) & 3u);
+#endif
 }
+
+// Frame mode: log2 of a wavefront's pixel rows (3: 8x8, 2: 16x4 — the default —, 1: 32x2) from
+// svo_cast_desc.flags (SVO_CAST_TILE_8X8 = 256, SVO_CAST_TILE_32X2 = 512), and wavefronts per
+// 8-pixel tile row
+SVO_HD int32_t frame_wave_lh(int32_t flags) { return (flags & 512) ? 1 : ((flags & 256) ? 3 : 2); }
+SVO_HD int32_t frame_wave_cols(int32_t width, int32_t lh) { return ((width + (1 << (6 - lh)) - 1) >> (6 - lh)) << (3 - lh); }
 
 // hit-record info word (see include/svo_rt.h)
 enum : uint32_t { HIT_BIT = 1u << 31, AXIS_SHIFT = 16, NEG_BIT = 1u << 18, MAT_MASK = 0xFFFFu };

@@ -1074,6 +1074,20 @@ extern "C" int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_
     return SVO_OK;
 }
 
+extern "C" int svo_cast_blocks(const svo_cast_desc* d, int64_t* n) {
+    if (!d || !n) SVO_FAIL(SVO_EINVAL, "svo_cast_blocks: NULL argument");
+    if (d->ray_dirs) {
+        *n = d->n_rays > 0 ? ((int64_t)d->n_rays + 63) / 64 : 0;
+        return SVO_OK;
+    }
+    if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0)
+        SVO_FAIL(SVO_EINVAL, "svo_cast_blocks: bad frame geometry");
+    const int32_t tile_rows = (d->height + 7) / 8;
+    const int64_t rows = d->tile_row_start < tile_rows ? (tile_rows - d->tile_row_start + d->tile_row_step - 1) / d->tile_row_step : 0;
+    *n = rows * svo::frame_wave_cols(d->width, svo::frame_wave_lh(d->flags));
+    return SVO_OK;
+}
+
 extern "C" int svo_cast_count(const svo_cast_desc* d, int64_t* n) {
     if (!d || !n) SVO_FAIL(SVO_EINVAL, "svo_cast_count: NULL argument");
     if (d->ray_dirs) {

@@ -65,7 +65,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     W = H = 256
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -196,6 +196,22 @@ def test_tile_row_sharding_reassembles(rt, torch_cuda, gtree):
                 assert np.array_equal(part[k], full[k][idx]), (G, r, k)
             rows[py] = True
         assert rows.all()
+
+
+def test_wavefront_footprints_ragged_frames(rt, gtree):
+    """8x8 / 32x2 wavefront footprints (scheduling only) write the same records as the default 16x4,
+    on frame sizes that are not multiples of the footprint, whole and sharded."""
+    org, d = CAMERAS[2]
+    dn = rt.normalize(d)
+    for W, H in ((100, 60), (33, 17), (8, 8)):
+        for start, step in ((0, 1), (1, 3)):
+            if start >= (H + 7) // 8:
+                continue  # an empty shard
+            base = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=start, tile_row_step=step))
+            for flags in (rt.CAST_TILE_8X8, rt.CAST_TILE_32X2):
+                got = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=start, tile_row_step=step, flags=flags))
+                for k in base:
+                    assert np.array_equal(got[k], base[k]), (W, H, start, step, flags, k)
 
 
 def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):

@@ -145,6 +145,22 @@ def test_cast_count_sharding(rt):
             assert sum(parts) == total
 
 
+def test_cast_blocks_per_footprint(rt):
+    """blocks (64-lane wavefronts) per launch: one per 16x4 footprint by default, 8x8 / 32x2 by flag,
+    one per 64 explicit rays; every block covers at most 64 rays"""
+    for W, H in ((1920, 1080), (33, 17), (8, 8), (100, 60)):
+        for step in (1, 3):
+            for start in range(step):
+                tile_rows = len(range(start, (H + 7) // 8, step))
+                for flags, tw in ((0, 16), (rt.CAST_TILE_8X8, 8), (rt.CAST_TILE_32X2, 32)):
+                    d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], W, H, 1, tile_row_start=start, tile_row_step=step, flags=flags)
+                    assert rt.Tree.blocks(d) == tile_rows * (8 * tw // 64) * ((W + tw - 1) // tw)
+                    assert rt.Tree.blocks(d) * 64 >= rt.Tree.count(d)
+    d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 8, 8, 1)
+    d.ray_dirs, d.n_rays = 1, 130  # explicit mode: only the count is read
+    assert rt.Tree.blocks(d) == 3
+
+
 def test_hemisphere_table_matches_reference_generator(rt, oracle_mod):
     g = json.load(open(os.path.join(GOLD, "hemisphere_ref.json")))
     py = np.array(g["generator_stdout"], np.float32)  # printed as (x, pole, y)
