@@ -76,13 +76,16 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #define SVO_UNIFORM_DIRS 1
 #endif
 #ifndef SVO_BRICK_PACK
-#define SVO_BRICK_PACK 2
+#define SVO_BRICK_PACK 3
 #endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
 #endif
 #ifndef SVO_FMA
 #define SVO_FMA 1
+#endif
+#ifndef SVO_P3_TLSTEP
+#define SVO_P3_TLSTEP 0  // A/B: brick walks keep the crossing value every step (one copy of the loop)
 #endif
 #ifndef SVO_VROOT
 #define SVO_VROOT 1  // start every ray below a virtual parent of the root (no first-lookup branch)
@@ -618,6 +621,55 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
 #endif
 }
 
+// (SVO_BRICK_PACK 3) One register holds the voxel index + 64 (bits 0-7), the steps left in the
+// brick per axis (nibbles at bits 8, 12, 16; at most 4) and the step budget min(steps, 2047) (bits
+// 20-30): one add per step updates them all and one test of the fields' guard bits ends the walk,
+// so a step carries no budget count, no axis and — when every ray of the wave is exact (TL_STEP
+// false; a wave-uniform choice between two copies of the loop) — no crossing value: the axis follows from the last step's delta, the crossing value
+// from T - absDelta on that axis (exact for such rays).  Returns the voxel index; left = the
+// per-axis nibbles.
+template <bool STATS, bool TL_STEP>
+__device__ __forceinline__ uint32_t brick_walk3(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
+                                                Stats& st) {
+    const uint32_t b0 = (uint32_t)max(0, min(R.steps, 2047));
+    uint32_t pk = (b0 << 20) | (left0 << 8) | (child_slot(w[0], w[1], w[2], 0u) + 64u);
+    const uint32_t d0 = (uint32_t)R.s[0] - 0x100100u, d1 = (uint32_t)(R.s[1] * 4) - 0x101000u, d2 = (uint32_t)(R.s[2] * 16) - 0x110000u;
+    solid = (bmask >> (pk & 63u)) & 1ull;
+    bool go = !solid && b0 > 0u;
+    uint32_t dl = 0u;
+    while (go) {  // one exit: the compiler keeps the state in place
+        // one DDA step (ray_caster.cpp:70-80) without position updates
+        const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+        const bool cy = !cx && (R.T[1] < R.T[2]);
+        const bool cz = !cx && !cy;
+        if (TL_STEP) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+        R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+        R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+        R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
+        dl = cx ? d0 : (cy ? d1 : d2);
+        pk += dl;
+        if (STATS) {
+            st.brick_steps++;
+            st.wv_brick += wave_lead();
+        }
+        const uint32_t zf = (pk - 0x111100u) & ~pk & 0x80088800u;  // guard bits of the fields now zero
+        solid = (zf & 0x88800u) == 0u && ((bmask >> (pk & 63u)) & 1ull);  // still inside: test the voxel
+        go = zf == 0u && !solid;
+    }
+    if (dl != 0u) {
+        const bool ax0 = dl == d0, ax1 = dl == d1;
+        R.axis = ax0 ? 0u : (ax1 ? 1u : 2u);
+        if (!TL_STEP) {
+            // (selects of values: a select of array elements becomes a scratch load)
+            const double t0 = R.T[0], t1 = R.T[1], t2 = R.T[2], a0 = R.a(0), a1 = R.a(1), a2 = R.a(2);
+            R.tlast = (float)(ax0 ? t0 - a0 : (ax1 ? t1 - a1 : t2 - a2));
+        }
+    }
+    R.steps -= (int32_t)(b0 - (pk >> 20));
+    left = (pk >> 8) & 0xFFFu;
+    return pk & 63u;
+}
+
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
 // direction after them, reflection count, finalColorMod, and whether the ray was bent.
 struct Bounce {
@@ -677,6 +729,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 exact_axis(R.T[2], R.a(2), budget);
     uint32_t ud[3];
     dir_flags(R.s, ud);
+    // every ray of the wave exact: brick walks recover crossing values afterwards (brick_walk3)
+    const bool allfast = !REFLECT && __ballot(fast) == __builtin_amdgcn_read_exec();
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -751,7 +805,38 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             pend = false;
             uint32_t w[3];
             wrap3(R, wm, w);
-#if SVO_BRICK_FAST
+#if SVO_BRICK_FAST && SVO_BRICK_PACK == 3
+            // Voxel index v, per-axis steps left in the brick and the budget are stepped in one
+            // register; positions follow from the step counts when the brick ends.
+            const uint32_t ex = R.s[0] > 0 ? 4u - (w[0] & 3u) : (w[0] & 3u) + 1u;
+            const uint32_t ey = R.s[1] > 0 ? 4u - (w[1] & 3u) : (w[1] & 3u) + 1u;
+            const uint32_t ez = R.s[2] > 0 ? 4u - (w[2] & 3u) : (w[2] & 3u) + 1u;
+            const uint32_t left0 = ex | (ey << 4) | (ez << 8);
+            uint32_t left, v;
+            bool solid;
+#if SVO_P3_TLSTEP
+            (void)allfast;
+            v = brick_walk3<STATS, true>(R, bmask, w, left0, left, solid, st);
+#else
+            if (allfast)
+                v = brick_walk3<STATS, false>(R, bmask, w, left0, left, solid, st);
+            else
+                v = brick_walk3<STATS, true>(R, bmask, w, left0, left, solid, st);
+#endif
+            if (solid) {
+                hit = true;
+                mat = brick_material(P, bmask, bref, binfo, v);
+                done = true;
+            } else if (R.steps <= 0 && (((left - 0x111u) & ~left & 0x888u) == 0u)) {
+                done = true;  // budget ended inside the brick
+            }
+            const int32_t nx = (int32_t)((left0 & 15u) - (left & 15u));
+            const int32_t ny = (int32_t)(((left0 >> 4) & 15u) - ((left >> 4) & 15u));
+            const int32_t nz = (int32_t)((left0 >> 8) - (left >> 8));
+            R.r[0] += R.s[0] > 0 ? nx : -nx;
+            R.r[1] += R.s[1] > 0 ? ny : -ny;
+            R.r[2] += R.s[2] > 0 ? nz : -nz;
+#elif SVO_BRICK_FAST
             // Voxel index v and per-axis steps left in the brick (one byte each) are stepped
             // instead of positions; positions follow from the step counts when the brick ends.
             const uint32_t ex = R.s[0] > 0 ? 4u - (w[0] & 3u) : (w[0] & 3u) + 1u;
