@@ -76,7 +76,7 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #define SVO_UNIFORM_DIRS 1
 #endif
 #ifndef SVO_BRICK_PACK
-#define SVO_BRICK_PACK 3
+#define SVO_BRICK_PACK 2  // 3: measured equal (brick_walk3), with a spill
 #endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
@@ -195,6 +195,13 @@ __device__ __forceinline__ void dir_flags(const int32_t s[3], uint32_t ud[3]) {
         const uint64_t b = __ballot(s[k] > 0);
         ud[k] = b == ex ? 1u : (b == 0ull ? 2u : 0u);
     }
+}
+
+// r + n or r - n by the step sign s; ud: wave-uniform sign (dir_flags) or 0
+__device__ __forceinline__ int32_t step_by(int32_t r, int32_t n, int32_t s, uint32_t ud) {
+    if (ud == 1u) return r + n;
+    if (ud == 2u) return r - n;
+    return s > 0 ? r + n : r - n;  // (s * n as a 24-bit multiply-add became v_mad_u64_u32)
 }
 
 #if SVO_BOX_V2
@@ -839,10 +846,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 #elif SVO_BRICK_FAST
             // Voxel index v and per-axis steps left in the brick (one byte each) are stepped
             // instead of positions; positions follow from the step counts when the brick ends.
-            const uint32_t ex = R.s[0] > 0 ? 4u - (w[0] & 3u) : (w[0] & 3u) + 1u;
-            const uint32_t ey = R.s[1] > 0 ? 4u - (w[1] & 3u) : (w[1] & 3u) + 1u;
-            const uint32_t ez = R.s[2] > 0 ? 4u - (w[2] & 3u) : (w[2] & 3u) + 1u;
-            const uint32_t left0 = ex | (ey << 8) | (ez << 16);
+            // Steps left: 4 - c stepping up, c + 1 stepping down (c = the cell in the brick), i.e.
+            // (c ^ 3) + 1 or c + 1 — all three bytes at once.
+            const uint32_t up3 = (R.s[0] > 0 ? 3u : 0u) | (R.s[1] > 0 ? 0x300u : 0u) | (R.s[2] > 0 ? 0x30000u : 0u);
+            const uint32_t left0 = (((w[0] & 3u) | ((w[1] & 3u) << 8) | ((w[2] & 3u) << 16)) ^ up3) + 0x010101u;
             uint32_t left, v;
             bool solid;
             v = brick_walk<STATS, true>(R, bmask, w, left0, left, solid, st);
@@ -853,12 +860,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             } else if (R.steps <= 0 && (((left - 0x010101u) & ~left & 0x808080u) == 0u)) {
                 done = true;  // budget ended inside the brick
             }
-            const int32_t nx = (int32_t)((left0 & 0xFFu) - (left & 0xFFu));
-            const int32_t ny = (int32_t)(((left0 >> 8) & 0xFFu) - ((left >> 8) & 0xFFu));
-            const int32_t nz = (int32_t)((left0 >> 16) - (left >> 16));
-            R.r[0] += R.s[0] > 0 ? nx : -nx;  // (s * n as a 24-bit multiply-add became v_mad_u64_u32)
-            R.r[1] += R.s[1] > 0 ? ny : -ny;
-            R.r[2] += R.s[2] > 0 ? nz : -nz;
+            const uint32_t dn = left0 - left;  // steps taken per axis, one byte each (no borrows)
+            R.r[0] = step_by(R.r[0], (int32_t)(dn & 0xFFu), R.s[0], REFLECT ? 0u : ud[0]);
+            R.r[1] = step_by(R.r[1], (int32_t)((dn >> 8) & 0xFFu), R.s[1], REFLECT ? 0u : ud[1]);
+            R.r[2] = step_by(R.r[2], (int32_t)(dn >> 16), R.s[2], REFLECT ? 0u : ud[2]);
 #else
             const uint32_t c[3] = {w[0], w[1], w[2]};
             for (;;) {
