@@ -116,6 +116,8 @@ def main():
                     help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray), "
                          "rgba gathered instead of hit records")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--verify", action="store_true",
+                    help="N>1: rank 0 checks the gathered, unpacked records of every frame against a one-GPU cast of it")
     ap.add_argument("--launch-events", action="store_true",
                     help="an event pair around every cast launch (default at N=1: one pair around the timed region, whose "
                          "average per launch includes the gaps between launches; per-launch pairs cost ~7 us per step)")
@@ -158,51 +160,96 @@ def main():
     from raytracing_test_amd import shard
 
     nframes = world
-    descs, flats, outs = [], [], []
-    # equal-size record buffers on every rank (RCCL gather): the largest shard, kernel writes in place
-    n_pad = shard.max_shard_count(W, H, world)
-    for f in range(nframes):
-        d = rt.Tree.frame_desc(frame_origin(f), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
-                               flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao)
-        descs.append(d)
-        flat, views = shard.alloc_flat(n_pad, torch.device("cuda", dev))
+    # one launch per step covers this rank's tile rows of all N frames (each frame's shard alone
+    # would fill 1/N of the GPU); records of frame f follow those of frame f-1
+    desc = rt.Tree.frame_desc(frame_origin(0), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
+                              flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao,
+                              frame_origins=[frame_origin(f) for f in range(nframes)] if nframes > 1 else None)
+    descs = [desc]
+    gather = world > 1 and not args.no_gather
+    # hit records travel as 12-B wire records (svo_hits_pack); the image (--shade) and the AO counts
+    # as they are
+    wire_fmt = gather and not args.shade and not args.ao
+    # equal-size buffers on every rank (RCCL gather): the largest shard; two sets so that the gather
+    # of step k overlaps the cast of step k+1
+    n_pad = shard.max_shard_count(W, H, world) * nframes
+    nbuf = 2 if gather else 1
+    gdev = torch.device("cuda", dev)
+    outs, payloads = [], []
+    for _ in range(nbuf):
+        flat, views = shard.alloc_flat(n_pad, gdev)
         if args.shade:  # the image is the product: gather it instead of the hit records
-            views["rgba"] = torch.zeros((n_pad, 4), dtype=torch.float32, device=torch.device("cuda", dev))
+            views["rgba"] = torch.zeros((n_pad, 4), dtype=torch.float32, device=gdev)
             flat = views["rgba"].view(-1)
         if args.ao:
-            views["ao"] = torch.zeros(n_pad, dtype=torch.uint8, device=torch.device("cuda", dev))
-        flats.append(flat)
+            views["ao"] = torch.zeros(n_pad, dtype=torch.uint8, device=gdev)
         outs.append(views)
+        payloads.append(torch.zeros((n_pad, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev) if wire_fmt else flat)
     stream = torch.cuda.Stream(device=dev)
-    gather_bufs = None
-    if world > 1 and not args.no_gather and rank == 0:
-        gather_bufs = [[torch.empty_like(flats[0]) for _ in range(world)] for _ in range(nframes)]
+    glists, glists_host, src_descs, src_hits = None, None, None, None
+    if gather and rank == 0:
+        glists = [[torch.empty_like(payloads[0]) for _ in range(world)] for _ in range(nbuf)]
+        if args.dist_backend != "nccl":  # gloo rehearsal: gathers through host copies
+            glists_host = [[torch.empty_like(payloads[0], device="cpu") for _ in range(world)] for _ in range(nbuf)]
+        if wire_fmt:  # rank 0 unpacks every rank's records (its tile rows of every frame)
+            src_descs = [rt.Tree.frame_desc(frame_origin(0), cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world,
+                                            frame_origins=[frame_origin(f) for f in range(nframes)]) for r in range(world)]
+            src_hits = [rt.Tree.alloc_hits(n_pad, dev) for _ in range(world)]
+    pending = {}  # step -> async gather work
 
-    def one_step(events=None):
+    def unpack_step(k):
+        """rank 0: wait (nccl: on the stream) for the gather of step k, then unpack every rank's records"""
+        pending.pop(k)[0].wait()
+        b = k % nbuf
+        for r in range(world):
+            if glists_host is not None:
+                glists[b][r].copy_(glists_host[b][r], non_blocking=False)
+            if wire_fmt:
+                tree.unpack_hits(src_descs[r], glists[b][r], src_hits[r], stream)
+
+    def one_step(k, events=None):
+        b = k % nbuf
         with torch.cuda.stream(stream):
-            for f in range(nframes):
-                if events is not None:
-                    events[f][0].record(stream)
-                if args.shade:
-                    tree.shade(descs[f], outs[f]["rgba"], out=outs[f], stream=stream)
-                else:
-                    tree.cast(descs[f], outs[f], stream)
-                if events is not None:
-                    events[f][1].record(stream)
-            if world > 1 and not args.no_gather:
-                for f in range(nframes):
-                    if args.dist_backend == "nccl":
-                        shard.gather_to_root(flats[f], rank, world, gather_bufs[f] if rank == 0 else None)
-                    else:  # gloo rehearsal: host copies
-                        shard.gather_to_root(flats[f].cpu(), rank, world, [b.cpu() for b in gather_bufs[f]] if rank == 0 else None)
+            if gather and rank != 0 and (k - nbuf) in pending:
+                pending.pop(k - nbuf)[0].wait()  # the gather that read this buffer set is done
+            if events is not None:
+                events[0][0].record(stream)
+            if args.shade:
+                tree.shade(desc, outs[b]["rgba"], out=outs[b], stream=stream)
+            else:
+                tree.cast(desc, outs[b], stream)
+            if events is not None:
+                events[0][1].record(stream)
+            if not gather:
+                return
+            if wire_fmt:
+                tree.pack_hits(desc, outs[b], payloads[b], stream)
+            # asynchronous: the next step's cast runs while RCCL moves this one over xGMI (gloo
+            # rehearsal: the same pipeline through host copies)
+            send = payloads[b] if glists_host is None and args.dist_backend == "nccl" else payloads[b].cpu()
+            recv = (glists[b] if args.dist_backend == "nccl" else glists_host[b]) if rank == 0 else None
+            pending[k] = (dist.gather(send, recv, dst=0, async_op=True), send)  # (keeps the send buffer alive)
+            if rank == 0 and (k - 1) in pending:
+                unpack_step(k - 1)
 
+    def drain():
+        with torch.cuda.stream(stream):
+            for k in sorted(pending):
+                if rank == 0:
+                    unpack_step(k)
+                else:
+                    pending.pop(k)[0].wait()
+
+    step_no = 0
     for _ in range(args.warmup):
-        one_step()
+        one_step(step_no)
+        step_no += 1
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(nframes)] for _ in range(args.steps)]
+    evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]] for _ in range(args.steps)]
     reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     # at N=1 the launches run back to back on one stream: one event pair around the timed region
     # gives their average (gaps included); with a gather in between, pairs around each launch
@@ -211,16 +258,18 @@ def main():
     if args.region_events:
         reg[0].record(stream)
     for k in range(args.steps):
-        one_step(None if args.region_events else evs[k])
+        one_step(step_no, None if args.region_events else evs[k])
+        step_no += 1
     if args.region_events:
         reg[1].record(stream)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if args.region_events:  # launches back to back on one stream (no gather in between at N=1)
-        kern_ms = [reg[0].elapsed_time(reg[1]) / (args.steps * nframes)]
+        kern_ms = [reg[0].elapsed_time(reg[1]) / args.steps]
     else:
         kern_ms = [e[0].elapsed_time(e[1]) for step in evs for e in step]
     if world > 1:
@@ -231,12 +280,24 @@ def main():
     value = total_rays / elapsed
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     rays_per_launch = rt.Tree.count(descs[0])
+    verified = None
+    if args.verify and rank == 0 and wire_fmt:
+        # every frame reassembled from the ranks' unpacked records == a one-GPU cast of the frame
+        verified = True
+        for f in range(nframes):
+            one = rt.decode_hits(tree.cast_frame(frame_origin(f), cam, W, H, STEPS, ppx, ppy, flags=args.cast_flags))
+            for r in range(world):
+                rows = shard.shard_pixel_rows(H, r, world)
+                n_r = len(rows) * W
+                got = rt.decode_hits({k: v[f * n_r:(f + 1) * n_r] for k, v in src_hits[r].items()})
+                idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+                verified &= all(np.array_equal(got[k], one[k][idx]) for k in ("pos", "steps", "hit", "axis", "material", "t"))
 
     if args.stats and rank == 0:
         d0 = descs[0]
         nblk = rt.Tree.blocks(d0)
         for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
-            st = torch.zeros(rt.STATS_HEADER + 2 * nblk + W * H, dtype=torch.int64, device=dev)
+            st = torch.zeros(rt.STATS_HEADER + 2 * nblk + rt.Tree.count(d0), dtype=torch.int64, device=dev)
             d0.flags |= mode
             d0.stats = st.data_ptr()
             tree.cast(d0, outs[0], stream)
@@ -303,11 +364,14 @@ def main():
                     "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols) +
                    " primary rays per GPU per step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % STEPS,
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
-                   "gather": world > 1 and not args.no_gather, "tree_nodes": info.n_nodes,
+                   "launches_per_step": 1, "gather": gather,
+                   "gather_payload": ("12-B wire hit records (svo_hits_pack), unpacked on rank 0" if wire_fmt else
+                                      ("rgba image" if args.shade else "24-B hit records + AO counts")) if gather else None, "tree_nodes": info.n_nodes,
                    "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
                    "tree_builder": "host" if args.host_build else "gpu"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        **({"gather_verified": verified} if verified is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
                          "included)" if args.region_events else "a HIP event pair around every launch on its stream",
     }

@@ -186,7 +186,15 @@ typedef struct {
                           then, with SVO_CAST_STATS in frame mode, one word per
                           output pixel: lookups | brick steps << 32
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
+    /* frame mode, several frames in one launch (the multi-GPU step: one launch per rank covers its
+       tile rows of every frame): n_frames <= SVO_MAX_FRAMES (0 or 1: one frame at `origin`);
+       frame_origins = host array of n_frames camera positions (origin is then ignored).  Records
+       of frame f follow those of frame f-1: svo_cast_count / svo_cast_blocks count all frames. */
+    int32_t n_frames;
+    const float* frame_origins;
 } svo_cast_desc;
+
+#define SVO_MAX_FRAMES 16
 
 /* svo_cast_desc.flags: take every DDA step one at a time (disables the exact closed-form crossing
    of empty regions; results are identical — for testing and A/B timing) */
@@ -220,6 +228,18 @@ int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* out
 int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* out,
                           svo_block* block);
 int svo_sync(void* hip_stream);
+
+/* Wire format of hit records for the exchange between GPUs (the tile-row gather), 12 B per ray:
+     int16 dx, dy, dz   pos - trunc(origin of the ray's frame, or of the explicit ray)
+     uint16 info16      hit << 15 | axis << 13 | (step < 0) << 12 | material id (12 bits)
+     float t
+   stepsLeft is not sent: every DDA step moves one axis by one voxel, so a hit leaves
+   steps - |dx| - |dy| - |dz| and a miss 0.  Needs steps <= 32767 and fewer than 4096 palette
+   entries (SVO_ERANGE otherwise).  d describes the records (svo_cast_count of them, the
+   frames / origins they were cast from); wire and hits are device buffers; asynchronous. */
+#define SVO_WIRE_BYTES 12
+int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const svo_hits* hits, void* wire, void* hip_stream);
+int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* hip_stream);
 
 /* ---------------------------------------------------------------------------- shading ------- */
 /* Shading pass: low_res.frag's colour model over castRayFromCam hits, one float4

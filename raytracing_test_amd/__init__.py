@@ -45,6 +45,8 @@ STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "bric
               "reserved16", "root_starts", "cache_empty", "wave_skips", "wave_descents",
               "path_starts")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
+MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
+WIRE_BYTES = 12  # SVO_WIRE_BYTES: one hit record in the exchange format (svo_hits_pack)
 
 
 class SvoError(RuntimeError):
@@ -100,6 +102,8 @@ class CastDesc(C.Structure):
         ("ao_samples", C.c_int32),
         ("ao_steps", C.c_int32),
         ("stats", C.c_void_p),
+        ("n_frames", C.c_int32),
+        ("frame_origins", C.c_void_p),
     ]
 
 
@@ -126,7 +130,7 @@ ABI_SYMBOLS = (
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
-    "svo_build_terrain_gpu", "svo_build_heightfield_gpu",
+    "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack",
 )
 
 
@@ -170,6 +174,8 @@ def lib():
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
     L.svo_cast_blocks.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
+    L.svo_hits_pack.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp, vp]
+    L.svo_hits_unpack.argtypes = [vp, C.POINTER(CastDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
     L.svo_shade_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(ShadeDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_ray_from_cam.argtypes = [vp, f3, f3, i32, C.POINTER(RayResult), C.POINTER(Block)]
@@ -442,10 +448,18 @@ class Tree:
     # ------------------------------------------------------------------------------ casting --
     @staticmethod
     def frame_desc(origin, cam_dir, width, height, steps, ppx=None, ppy=None, tile_row_start=0, tile_row_step=1, flags=0,
-                   ao_samples=0, ao_steps=5):
+                   ao_samples=0, ao_steps=5, frame_origins=None):
+        """frame_origins: several frames (camera positions) in one launch; records of frame f
+        follow those of frame f-1 (origin is then ignored)"""
         if ppx is None:
             ppx, ppy = proj_plane(width, height)
         d = CastDesc()
+        if frame_origins is not None and len(frame_origins) > 0:
+            fo = np.ascontiguousarray(np.asarray(frame_origins, np.float32).reshape(-1, 3))
+            d._frame_origins = fo  # keep the host array alive with the desc
+            d.n_frames = len(fo)
+            d.frame_origins = fo.ctypes.data
+            origin = fo[0]
         d.origin[:] = [float(x) for x in origin]
         d.cam_dir[:] = [float(x) for x in cam_dir]
         d.width, d.height, d.ppx, d.ppy = width, height, ppx, ppy
@@ -481,6 +495,20 @@ class Tree:
         if ao:
             out["ao"] = torch.empty(n, dtype=torch.uint8, device=dev)
         return out
+
+    def pack_hits(self, desc, out, wire, stream=None):
+        """hit records (device) -> the 12-B wire records of include/svo_rt.h in `wire` (uint8 tensor)"""
+        h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), None)
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_hits_pack(self._h, C.byref(desc), C.byref(h), C.c_void_p(wire.data_ptr()), C.c_void_p(s) if s else None),
+               "svo_hits_pack")
+
+    def unpack_hits(self, desc, wire, out, stream=None):
+        """12-B wire records -> hit records (device)"""
+        h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), None)
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_hits_unpack(self._h, C.byref(desc), C.c_void_p(wire.data_ptr()), C.byref(h), C.c_void_p(s) if s else None),
+               "svo_hits_unpack")
 
     def cast(self, desc, out, stream=None):
         """Launch the cast kernel asynchronously on `stream` (a torch.cuda.Stream or raw handle)."""

@@ -42,6 +42,9 @@ struct CastParams {
     float sdir[3];
     int32_t width, height, tiles_x, tile_row_start, tile_row_step, tile_rows_local;
     int32_t tile_lh;  // log2 of a wavefront's pixel rows (frame_wave_lh)
+    int32_t n_frames;        // frames in this launch (>= 1); frame f casts from frame_org[3f..]
+    int64_t frame_records;   // records of one frame (this shard)
+    float frame_org[3 * SVO_MAX_FRAMES];
     // explicit mode
     const float* rdir;
     const float* rorg;
@@ -737,7 +740,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     uint32_t ud[3];
     dir_flags(R.s, ud);
     // every ray of the wave exact: brick walks recover crossing values afterwards (brick_walk3)
+#if SVO_BRICK_PACK == 3
     const bool allfast = !REFLECT && __ballot(fast) == __builtin_amdgcn_read_exec();
+#endif
     bool hit = false;
     uint32_t mat = 0u;
     const uint32_t wm = P.wmask;
@@ -1134,7 +1139,10 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
     if (P.mode == MODE_FRAME) {
         // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes.
         // The tile index is wave-uniform: its division runs on the scalar unit.
-        const uint32_t tile = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        // frames interleave wave by wave (every frame's long top rows first); the frame and tile
+        // indices are wave-uniform: their divisions run on the scalar unit
+        const uint32_t wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
         const int32_t lane = (int32_t)(threadIdx.x & 63u);
         const uint32_t tq = tile / (uint32_t)P.tiles_x;
         int32_t trl = (int32_t)tq;
@@ -1150,10 +1158,10 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
         if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
-            o[0] = P.org[0];
-            o[1] = P.org[1];
-            o[2] = P.org[2];
-            out = ((int64_t)trl * 8 + rr) * P.width + px;
+            o[0] = P.frame_org[3 * fr + 0];
+            o[1] = P.frame_org[3 * fr + 1];
+            o[2] = P.frame_org[3 * fr + 2];
+            out = (int64_t)fr * P.frame_records + ((int64_t)trl * 8 + rr) * P.width + px;
         }
     } else if (P.mode == MODE_EXPLICIT) {
         if (g < P.n_rays) {
@@ -1400,9 +1408,17 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.tile_row_step = d->tile_row_step;
     const int32_t tile_rows = (d->height + 7) / 8;
     P.tile_rows_local = d->tile_row_start < tile_rows ? (tile_rows - d->tile_row_start + d->tile_row_step - 1) / d->tile_row_step : 0;
-    if ((int64_t)P.tile_rows_local * P.tiles_x >= (int64_t)1 << 31)
-        SVO_FAIL(SVO_EINVAL, "svo_cast_rays: frame too large (2^31 tiles of 8x8 pixels or more)");
-    nthreads = (int64_t)P.tile_rows_local * P.tiles_x * 64;
+    if (d->n_frames < 0 || d->n_frames > SVO_MAX_FRAMES) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: n_frames outside [0, SVO_MAX_FRAMES]");
+    if (d->n_frames > 1 && !d->frame_origins) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: n_frames > 1 without frame_origins");
+    P.n_frames = d->n_frames > 1 ? d->n_frames : 1;
+    for (int32_t f = 0; f < P.n_frames; f++)
+        for (int k = 0; k < 3; k++) P.frame_org[3 * f + k] = d->n_frames > 1 ? d->frame_origins[3 * f + k] : d->origin[k];
+    int64_t per_frame = 0;
+    for (int32_t r = d->tile_row_start; r < tile_rows; r += d->tile_row_step) per_frame += std::min(8, d->height - r * 8);
+    P.frame_records = per_frame * d->width;
+    if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 31)
+        SVO_FAIL(SVO_EINVAL, "svo_cast_rays: frame too large (2^31 wavefronts or more)");
+    nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
     return SVO_OK;
 }
 
@@ -1661,5 +1677,116 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
 
 extern "C" int svo_sync(void* stream) {
     HIP_TRY(hipStreamSynchronize((hipStream_t)stream), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+// ================================================================================================
+// wire format of hit records for the tile-row gather (include/svo_rt.h: 12 B per ray)
+// ================================================================================================
+namespace {
+
+struct WireParams {
+    int64_t n, frame_records;
+    int32_t explicit_mode, steps;
+    float frame_org[3 * SVO_MAX_FRAMES];
+    const float* rorg;  // explicit rays: per-ray origins (or null: frame_org[0..2])
+    int32_t* pos;
+    float* t;
+    uint32_t* info;
+    uint32_t* wire;
+};
+
+// trunc of the origin the record's ray started from (dda_axis: round = trunc(origin))
+__device__ __forceinline__ void record_origin_cell(const WireParams& Q, int64_t i, int32_t c[3]) {
+    if (Q.explicit_mode && Q.rorg) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) c[k] = (int32_t)__builtin_truncf(Q.rorg[3 * i + k]);
+    } else {
+        const int64_t f = Q.explicit_mode ? 0 : i / Q.frame_records;
+#pragma unroll
+        for (int k = 0; k < 3; k++) c[k] = (int32_t)__builtin_truncf(Q.frame_org[3 * f + k]);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hits_pack(const WireParams Q) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= Q.n) return;
+    int32_t c[3];
+    record_origin_cell(Q, i, c);
+    const int4 ps = reinterpret_cast<const int4*>(Q.pos)[i];
+    const uint32_t inf = Q.info[i];
+    const uint32_t i16 = ((inf >> 31) << 15) | (((inf >> AXIS_SHIFT) & 3u) << 13) | (((inf & NEG_BIT) ? 1u : 0u) << 12) | (inf & 0xFFFu);
+    const uint32_t dx = (uint32_t)(ps.x - c[0]) & 0xFFFFu, dy = (uint32_t)(ps.y - c[1]) & 0xFFFFu, dz = (uint32_t)(ps.z - c[2]) & 0xFFFFu;
+    uint32_t* w = Q.wire + 3 * i;
+    w[0] = dx | (dy << 16);
+    w[1] = dz | (i16 << 16);
+    w[2] = __float_as_uint(Q.t[i]);
+}
+
+__global__ __launch_bounds__(256) void k_hits_unpack(const WireParams Q) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= Q.n) return;
+    int32_t c[3];
+    record_origin_cell(Q, i, c);
+    const uint32_t* w = Q.wire + 3 * i;
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const int32_t dx = (int32_t)(int16_t)(w0 & 0xFFFFu), dy = (int32_t)(int16_t)(w0 >> 16), dz = (int32_t)(int16_t)(w1 & 0xFFFFu);
+    const uint32_t i16 = w1 >> 16;
+    const bool hit = (i16 >> 15) != 0u;
+    // one voxel per DDA step on one axis: a hit used |dx| + |dy| + |dz| steps, a miss all of them
+    const int32_t left = hit ? Q.steps - (abs(dx) + abs(dy) + abs(dz)) : 0;
+    reinterpret_cast<int4*>(Q.pos)[i] = make_int4(c[0] + dx, c[1] + dy, c[2] + dz, left);
+    Q.t[i] = __uint_as_float(w2);
+    Q.info[i] = (hit ? HIT_BIT : 0u) | (((i16 >> 13) & 3u) << AXIS_SHIFT) | (((i16 >> 12) & 1u) ? NEG_BIT : 0u) | (i16 & 0xFFFu);
+}
+
+int wire_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* h, const char* fn, WireParams& Q) {
+    if (!t || !d || !h || !h->pos_steps || !h->t || !h->info) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL argument");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, std::string(fn) + ": tree not uploaded (svo_upload)");
+    if (d->steps < 0 || d->steps > 32767) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire format needs steps <= 32767");
+    if (t->palette.size() > 4096) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire format needs fewer than 4096 materials");
+    memset(&Q, 0, sizeof(Q));
+    int64_t n = 0;
+    int rc = svo_cast_count(d, &n);
+    if (rc) return rc;
+    Q.n = n;
+    Q.steps = d->steps;
+    Q.explicit_mode = d->ray_dirs != nullptr;
+    const int32_t nf = (!Q.explicit_mode && d->n_frames > 1) ? d->n_frames : 1;
+    Q.frame_records = n / nf;
+    for (int32_t f = 0; f < nf; f++)
+        for (int k = 0; k < 3; k++) Q.frame_org[3 * f + k] = nf > 1 ? d->frame_origins[3 * f + k] : d->origin[k];
+    Q.rorg = Q.explicit_mode ? d->ray_origins : nullptr;
+    Q.pos = h->pos_steps;
+    Q.t = h->t;
+    Q.info = h->info;
+    return SVO_OK;
+}
+
+}  // namespace
+
+extern "C" int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const svo_hits* hits, void* wire, void* stream) {
+    WireParams Q;
+    int rc = wire_params(t, d, hits, "svo_hits_pack", Q);
+    if (rc) return rc;
+    if (!wire) SVO_FAIL(SVO_EINVAL, "svo_hits_pack: NULL wire buffer");
+    Q.wire = reinterpret_cast<uint32_t*>(wire);
+    if (Q.n == 0) return SVO_OK;
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    hipLaunchKernelGGL(k_hits_pack, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Q);
+    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+extern "C" int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* stream) {
+    WireParams Q;
+    int rc = wire_params(t, d, hits, "svo_hits_unpack", Q);
+    if (rc) return rc;
+    if (!wire) SVO_FAIL(SVO_EINVAL, "svo_hits_unpack: NULL wire buffer");
+    Q.wire = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(wire));
+    if (Q.n == 0) return SVO_OK;
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    hipLaunchKernelGGL(k_hits_unpack, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Q);
+    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }

@@ -1074,6 +1074,14 @@ extern "C" int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_
     return SVO_OK;
 }
 
+// frames of a frame-mode desc (validated: 1 .. SVO_MAX_FRAMES, origins given for more than one)
+static int desc_frames(const svo_cast_desc* d, const char* fn, int32_t* nf) {
+    *nf = d->n_frames <= 1 ? 1 : d->n_frames;
+    if (d->n_frames < 0 || d->n_frames > SVO_MAX_FRAMES) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": n_frames outside [0, SVO_MAX_FRAMES]");
+    if (d->n_frames > 1 && !d->frame_origins) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": n_frames > 1 without frame_origins");
+    return SVO_OK;
+}
+
 extern "C" int svo_cast_blocks(const svo_cast_desc* d, int64_t* n) {
     if (!d || !n) SVO_FAIL(SVO_EINVAL, "svo_cast_blocks: NULL argument");
     if (d->ray_dirs) {
@@ -1082,9 +1090,12 @@ extern "C" int svo_cast_blocks(const svo_cast_desc* d, int64_t* n) {
     }
     if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0)
         SVO_FAIL(SVO_EINVAL, "svo_cast_blocks: bad frame geometry");
+    int32_t nf = 1;
+    int rc = desc_frames(d, "svo_cast_blocks", &nf);
+    if (rc) return rc;
     const int32_t tile_rows = (d->height + 7) / 8;
     const int64_t rows = d->tile_row_start < tile_rows ? (tile_rows - d->tile_row_start + d->tile_row_step - 1) / d->tile_row_step : 0;
-    *n = rows * svo::frame_wave_cols(d->width, svo::frame_wave_lh(d->flags));
+    *n = rows * svo::frame_wave_cols(d->width, svo::frame_wave_lh(d->flags)) * nf;
     return SVO_OK;
 }
 
@@ -1096,9 +1107,12 @@ extern "C" int svo_cast_count(const svo_cast_desc* d, int64_t* n) {
     }
     if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0)
         SVO_FAIL(SVO_EINVAL, "svo_cast_count: bad frame geometry");
+    int32_t nf = 1;
+    int rc = desc_frames(d, "svo_cast_count", &nf);
+    if (rc) return rc;
     const int32_t tile_rows = (d->height + 7) / 8;
     int64_t rows = 0;
     for (int32_t r = d->tile_row_start; r < tile_rows; r += d->tile_row_step) rows += std::min(8, d->height - r * 8);
-    *n = rows * d->width;
+    *n = rows * d->width * nf;
     return SVO_OK;
 }

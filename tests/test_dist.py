@@ -77,6 +77,80 @@ def test_tile_row_shard_gather_reassemble(world):
         assert np.array_equal(full[k], want[k].numpy()), k
 
 
+def _wire_worker(rank, world, port, W, H, origins, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    import wire_ref
+    from oracle import oracle as O
+    from raytracing_test_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    T = O.Tree.reference_world()
+    cam = O.normalize([1, -0.45, 1])
+    rows = shard.shard_pixel_rows(H, rank, world)
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+    # one multi-frame record buffer per rank: its tile rows of every frame, frame after frame
+    parts = []
+    for org in origins:
+        ref = T.cast_frame(org, cam, W, H, 300, pixels=pix, nthreads=2)
+        r = _records(ref, np.arange(len(pix)))
+        cell = np.trunc(np.asarray(org, np.float32)).astype(np.int32)
+        parts.append(wire_ref.pack(r["pos_steps"].numpy(), r["t"].numpy(), r["info"].numpy().view(np.uint32), cell[None, :]))
+    n_pad = shard.max_shard_count(W, H, world) * len(origins)
+    wire = torch.zeros((n_pad, 12), dtype=torch.uint8)
+    mine = np.concatenate(parts)
+    wire[: len(mine)] = torch.from_numpy(mine)
+    got = shard.gather_to_root(wire, rank, world)
+    if rank == 0:
+        q.put([g.numpy().copy() for g in got])
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wire_gather_multi_frame(world):
+    """The N>1 step: each rank packs its tile rows of several frames into 12-B wire records, rank 0
+    gathers and unpacks them; every frame equals its single-rank cast record for record."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wire_ref
+    from oracle import oracle as O
+    from raytracing_test_amd import shard
+
+    W, H = 64, 44  # 6 tile rows, the last one partial
+    origins = [(4.0, 90.0, 4.0), (68.0, 90.0, 68.0), (-30.5, 70.25, 12.75)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_wire_worker, args=(r, world, port, W, H, origins, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    T = O.Tree.reference_world()
+    cam = O.normalize([1, -0.45, 1])
+    for f, org in enumerate(origins):
+        ref = T.cast_frame(org, cam, W, H, 300)
+        want = _records(ref, np.arange(W * H))
+        cell = np.trunc(np.asarray(org, np.float32)).astype(np.int32)[None, :]
+        full = {k: np.zeros_like(v.numpy()) for k, v in want.items()}
+        for r in range(world):
+            rows = shard.shard_pixel_rows(H, r, world)
+            n = len(rows) * W
+            ps_, t_, info_ = wire_ref.unpack(got[r][f * n:(f + 1) * n], cell, 300)
+            idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+            full["pos_steps"][idx], full["t"][idx], full["info"][idx] = ps_, t_, info_.view(np.int32)
+        for k in want:
+            assert np.array_equal(full[k], want[k].numpy()), (f, k)
+
+
 def test_shard_geometry():
     sys.path.insert(0, ROOT)
     from raytracing_test_amd import shard

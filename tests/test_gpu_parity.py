@@ -214,6 +214,76 @@ def test_wavefront_footprints_ragged_frames(rt, gtree):
                     assert np.array_equal(got[k], base[k]), (W, H, start, step, flags, k)
 
 
+def test_multi_frame_launch(rt, torch_cuda, gtree):
+    """Several frames (camera positions) in one launch, whole and sharded: frame f's records equal
+    a single-frame cast of it; the AO counts and the shading pass follow the same layout."""
+    _, d = CAMERAS[1]
+    dn = rt.normalize(d)
+    origins = [(4.0, 90.0, 4.0), (68.0, 90.0, 68.0), (-30.5, 70.25, 12.75), (150.3, 44.7, 20.9)]
+    W, H = 72, 44
+    for start, step in ((0, 1), (1, 3)):
+        desc = rt.Tree.frame_desc(origins[0], dn, W, H, 300, tile_row_start=start, tile_row_step=step, frame_origins=origins,
+                                  ao_samples=16, ao_steps=5)
+        n = rt.Tree.count(desc)
+        out = rt.Tree.alloc_hits(n, 0, ao=True)
+        gtree.cast(desc, out)
+        torch_cuda.cuda.synchronize()
+        multi = rt.decode_hits(out)
+        per = n // len(origins)
+        for f, org in enumerate(origins):
+            one = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=start, tile_row_step=step, ao_samples=16))
+            for k in one:
+                assert np.array_equal(multi[k][f * per:(f + 1) * per], one[k]), (start, step, f, k)
+
+
+def test_wire_pack_roundtrip(rt, torch_cuda, gtree):
+    """svo_hits_pack / svo_hits_unpack (the exchange format of the tile-row gather) against the
+    numpy restatement in tests/wire_ref.py, and unpack(pack(records)) == records: hits and misses
+    (budget 30), several frames, explicit rays with their own origins."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import wire_ref
+
+    torch = torch_cuda
+    _, d = CAMERAS[0]
+    dn = rt.normalize(d)
+    origins = [(35.0, 50.0, 35.0), (-3.5, 40.25, -2.75), (1020.5, 35.5, 50.5)]
+    for steps in (30, 300):
+        desc = rt.Tree.frame_desc(origins[0], dn, 64, 40, steps, frame_origins=origins)
+        n = rt.Tree.count(desc)
+        out = rt.Tree.alloc_hits(n, 0)
+        gtree.cast(desc, out)
+        wire = torch.zeros((n, rt.WIRE_BYTES), dtype=torch.uint8, device="cuda")
+        gtree.pack_hits(desc, out, wire)
+        back = rt.Tree.alloc_hits(n, 0)
+        gtree.unpack_hits(desc, wire, back)
+        torch.cuda.synchronize()
+        cells = np.repeat(np.trunc(np.asarray(origins, np.float32)).astype(np.int32), n // len(origins), 0)
+        ps, t, info = out["pos_steps"].cpu().numpy(), out["t"].cpu().numpy(), out["info"].cpu().numpy().view(np.uint32)
+        assert np.array_equal(wire.cpu().numpy(), wire_ref.pack(ps, t, info, cells)), steps
+        for k in ("pos_steps", "t", "info"):
+            assert np.array_equal(back[k].cpu().numpy(), out[k].cpu().numpy()), (steps, k)
+        g = rt.decode_hits(out)
+        assert 0 < g["hit"].sum() < n or steps == 300  # both kinds of records at the small budget
+    rng = np.random.default_rng(3)
+    org = np.stack([rng.uniform(-50, 250, 500), rng.uniform(0, 120, 500), rng.uniform(-50, 250, 500)], 1).astype(np.float32)
+    dr = rng.normal(size=(500, 3)).astype(np.float32)
+    dr /= np.linalg.norm(dr, axis=1, keepdims=True)
+    go, gd = torch.from_numpy(org).cuda(), torch.from_numpy(dr).cuda()
+    out = gtree.cast_rays(gd, go, steps=300)
+    desc = rt.CastDesc()
+    desc.ray_dirs, desc.ray_origins, desc.n_rays, desc.steps = gd.data_ptr(), go.data_ptr(), 500, 300
+    wire = torch.zeros((500, rt.WIRE_BYTES), dtype=torch.uint8, device="cuda")
+    gtree.pack_hits(desc, out, wire)
+    back = rt.Tree.alloc_hits(500, 0)
+    gtree.unpack_hits(desc, wire, back)
+    torch.cuda.synchronize()
+    for k in ("pos_steps", "t", "info"):
+        assert np.array_equal(back[k].cpu().numpy(), out[k].cpu().numpy()), k
+
+
 def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):
     """Config C1: the reference world's [0,256)^3 as a dense grid (coordinates & 255) on the CPU
     oracle vs the same voxels in a 4-level tree on the GPU."""
