@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SVO_RT_VERSION 1
+#define SVO_RT_VERSION 2  /* 2: svo_cast_desc.n_frames / frame_origins, wire records */
 
 enum {
     SVO_OK = 0,
