@@ -40,15 +40,19 @@ STEPS = 16384
 B_OUT = 24  # hit record bytes per ray (int4 pos+steps, f32 t, u32 info)
 
 
+FRAME_SHIFT = 64.0  # camera shift along the diagonal between the frames of one step (N > 1)
+BRAY_KEY = {"c2": "C2_cam1_S300", "c2cam0": "C2_cam0_S300", "c3": "C3", "c5": "C5"}
+
+
 def frame_origin(f):
-    return (ORIGIN[0] + 64.0 * f, ORIGIN[1], ORIGIN[2] + 64.0 * f)
+    return (ORIGIN[0] + FRAME_SHIFT * f, ORIGIN[1], ORIGIN[2] + FRAME_SHIFT * f)
 
 
 def load_bray(config="c3"):
     p = os.path.join(ROOT, "profiles", "bray.json")
     if os.path.exists(p):
         d = json.load(open(p))
-        c = d.get(config.upper())
+        c = d.get(BRAY_KEY[config])
         if c:
             return c["e_child_per_ray"], d
     return None, None
@@ -62,14 +66,14 @@ def load_traffic():
     return None, None
 
 
-def cpu_baseline(ppx, ppy, gpu_hits=None):
+def cpu_baseline(ppx, ppy, gpu_hits=None, config="c3"):
     """Oracle (test infrastructure) timed on the host: the reference algorithm and layout."""
     from oracle import oracle as O
 
     O.build(native=True)
     cores = min(16, os.cpu_count() or 1)
     t0 = time.time()
-    T = O.Tree.terrain(LEVELS, COLS, COLS, native=True, nthreads=cores)
+    T = O.Tree.reference_world() if config.startswith("c2") else O.Tree.terrain(LEVELS, COLS, COLS, native=True, nthreads=cores)
     build_s = time.time() - t0
     dn = O.normalize(CAM)
     rng = np.random.default_rng(1)
@@ -86,8 +90,8 @@ def cpu_baseline(ppx, ppy, gpu_hits=None):
         "unit": "rays/s",
         "cores": cores,
         "kind": "port",
-        "sample": "%d random pixels (1/4) of the same 1080p C3 frame, %d threads; oracle/oracle.c (-O3 -march=native "
-                  "-ffp-contract=off) restating castRayFromCam + getBlock on the reference node/array layout" % (len(pix), cores),
+        "sample": "%d random pixels (1/4) of the same 1080p %s frame, %d threads; oracle/oracle.c (-O3 -march=native "
+                  "-ffp-contract=off) restating castRayFromCam + getBlock on the reference node/array layout" % (len(pix), config.upper(), cores),
         "single_thread_rays_per_s": len(one) / dt1,
         "tree_build_s": round(build_s, 2),
     }
@@ -105,8 +109,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--cols", type=int, default=None)
-    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
-                    help="c3: depth-12 / 1080p (the metric); c5: depth-14 (16384^2 columns, 7 levels) / 3840x2160")
+    ap.add_argument("--config", default="c3", choices=["c2", "c2cam0", "c3", "c5"],
+                    help="c3: depth-12 / 1080p (the metric); c5: depth-14 (16384^2 columns, 7 levels) / 3840x2160; c2: the "
+                         "reference world (initTetraHexaTree + genWorld, 5 levels) / 1080p / S=300 from the C3 pose, c2cam0 "
+                         "from the reference's default camera")
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
@@ -139,14 +145,22 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
 
-    global LEVELS, W, H
+    global LEVELS, W, H, ORIGIN, CAM, STEPS, FRAME_SHIFT
+    if args.config.startswith("c2"):
+        LEVELS, STEPS, FRAME_SHIFT = 5, 300, 8.0
+        if args.config == "c2cam0":  # globals.cpp:20-21
+            ORIGIN, CAM = (35.0, 50.0, 35.0), (1.0, 0.0, 1.0)
     if args.config == "c5":
         LEVELS, W, H = 7, 3840, 2160
         args.no_cpu_baseline = True  # the reference-format CPU tree of 16384^2 terrain exceeds its 2^32-byte pools
     if args.cols is None:
         args.cols = 4096 if args.config == "c3" else 16384
     t0 = time.time()
-    if args.host_build:
+    if args.config.startswith("c2"):  # initTetraHexaTree + genWorld, putBlock by putBlock
+        tree = rt.World.reference().build()
+        build_s = time.time() - t0
+        tree.upload(dev)
+    elif args.host_build:
         tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
         build_s = time.time() - t0
         tree.upload(dev)
@@ -342,10 +356,13 @@ def main():
         roof = None  # the roofline model (§8d) prices primary traversal only
     if world == 1 and not args.no_cpu_baseline and not args.ao and not args.shade:
         hits = rt.decode_hits(outs[0])
-        cpu = cpu_baseline(ppx, ppy, hits)
+        cpu = cpu_baseline(ppx, ppy, hits, args.config)
     line = {
         "metric": ("shaded primary rays/sec (reflections + sun shadow ray)" if args.shade else
-                   "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
+                   {"c2": "primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline",
+                    "c2cam0": "primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline",
+                    "c3": "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline",
+                    "c5": "primary rays/sec at 4K, depth-14 SVO; achieved HBM GB/s vs roofline"}[args.config]),
         "value": round(value, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -356,13 +373,18 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols),
+        "data": ("synthetic: the reference world (initTetraHexaTree + genWorld on 200x200 columns), built in-process"
+                 if args.config.startswith("c2") else
+                 "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols)),
         "config": {"ao_samples": args.ao, "shade": args.shade,
                    "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") +
                    ("shaded (low_res.frag colour model, 75-step shadow rays): " if args.shade else "") +
-                   ("C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080" % args.cols if args.config == "c3" else
-                    "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols) +
-                   " primary rays per GPU per step, camera (4,90,4)->normalize(1,-0.45,1), S=%d, castRayFromCam semantics" % STEPS,
+                   {"c2": "C2: the reference world (5 levels, 1024^3), 1920x1080",
+                    "c2cam0": "C2: the reference world (5 levels, 1024^3), 1920x1080",
+                    "c3": "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080" % args.cols,
+                    "c5": "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols}[args.config] +
+                   " primary rays per GPU per step, camera (%g,%g,%g)->normalize(%g,%g,%g), S=%d, castRayFromCam semantics"
+                   % (ORIGIN + CAM + (STEPS,)),
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
                    "launches_per_step": 1, "gather": gather,
                    "gather_payload": ("12-B wire hit records (svo_hits_pack), unpacked on rank 0" if wire_fmt else
