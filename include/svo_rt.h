@@ -217,6 +217,9 @@ typedef struct {
    covers 16x4 pixels of its 8-pixel tile row; these bits select 8x8 or 32x2 instead */
 #define SVO_CAST_TILE_8X8 256
 #define SVO_CAST_TILE_32X2 512
+/* svo_cast_desc.flags, scheduling (results identical): dispatch tile rows in order of the vertical
+   slope of their centre ray, shallowest first (grazing rays travel furthest over terrain) */
+#define SVO_CAST_HORIZON_FIRST 1024
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

@@ -39,6 +39,7 @@ CAST_TIMELINE = 32  # per-block start/end stamps only
 CAST_AO_TRACE = 128  # AO: trace every AO ray instead of the per-face voxel plan (A/B reference)
 CAST_TILE_8X8 = 256  # scheduling: one wavefront per 8x8 tile (default: 16x4 pixels of its 8-pixel tile row)
 CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel tile row
+CAST_HORIZON_FIRST = 1024  # scheduling: tile rows with the shallowest centre ray first
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",

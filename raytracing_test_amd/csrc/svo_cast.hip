@@ -27,6 +27,8 @@ namespace {
 
 enum : int32_t { MODE_FRAME = 0, MODE_EXPLICIT = 1, MODE_SINGLE = 2 };
 
+constexpr int kMaxOrderRows = 512;   // local tile rows a dispatch order is kept for (4K: 270)
+
 struct CastParams {
     const Node* nodes;
     const uint16_t* mats;
@@ -45,6 +47,8 @@ struct CastParams {
     int32_t n_frames;        // frames in this launch (>= 1); frame f casts from frame_org[3f..]
     int64_t frame_records;   // records of one frame (this shard)
     float frame_org[3 * SVO_MAX_FRAMES];
+    int32_t use_row_order;                // dispatch order of the local tile rows (else top first)
+    uint16_t row_order[kMaxOrderRows];
     // explicit mode
     const float* rdir;
     const float* rorg;
@@ -1148,7 +1152,8 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
         int32_t trl = (int32_t)tq;
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
-        if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
+        if (P.use_row_order) trl = P.row_order[tq];
+        else if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
@@ -1419,6 +1424,19 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 31)
         SVO_FAIL(SVO_EINVAL, "svo_cast_rays: frame too large (2^31 wavefronts or more)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
+    if ((d->flags & SVO_CAST_HORIZON_FIRST) && P.tile_rows_local <= kMaxOrderRows) {
+        // shallowest centre ray first (a stable sort of the local rows by |dir.y| of their middle pixel)
+        std::vector<std::pair<float, int32_t>> key(P.tile_rows_local);
+        for (int32_t i = 0; i < P.tile_rows_local; i++) {
+            const int32_t tr = P.tile_row_start + i * P.tile_row_step;
+            float dir[3];
+            raygen_pixel(P.rg, d->width / 2, std::min(tr * 8 + 4, d->height - 1), dir);
+            key[i] = {dir[1] < 0.0f ? -dir[1] : dir[1], i};
+        }
+        std::stable_sort(key.begin(), key.end(), [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) { return a.first < b.first; });
+        for (int32_t i = 0; i < P.tile_rows_local; i++) P.row_order[i] = (uint16_t)key[i].second;
+        P.use_row_order = 1;
+    }
     return SVO_OK;
 }
 

@@ -65,7 +65,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     W = H = 256
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -208,7 +208,7 @@ def test_wavefront_footprints_ragged_frames(rt, gtree):
             if start >= (H + 7) // 8:
                 continue  # an empty shard
             base = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=start, tile_row_step=step))
-            for flags in (rt.CAST_TILE_8X8, rt.CAST_TILE_32X2):
+            for flags in (rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST, rt.CAST_HORIZON_FIRST | rt.CAST_TILE_8X8):
                 got = rt.decode_hits(gtree.cast_frame(org, dn, W, H, 300, tile_row_start=start, tile_row_step=step, flags=flags))
                 for k in base:
                     assert np.array_equal(got[k], base[k]), (W, H, start, step, flags, k)
