@@ -176,56 +176,71 @@ def main():
     nframes = world
     # one launch per step covers this rank's tile rows of all N frames (each frame's shard alone
     # would fill 1/N of the GPU); records of frame f follow those of frame f-1
-    desc = rt.Tree.frame_desc(frame_origin(0), cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
+    origins = [frame_origin(f) for f in range(nframes)]
+    desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
                               flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao,
-                              frame_origins=[frame_origin(f) for f in range(nframes)] if nframes > 1 else None)
+                              frame_origins=origins if nframes > 1 else None)
     descs = [desc]
     gather = world > 1 and not args.no_gather
-    # hit records travel as 12-B wire records (svo_hits_pack); the image (--shade) and the AO counts
-    # as they are
-    wire_fmt = gather and not args.shade and not args.ao
-    # equal-size buffers on every rank (RCCL gather): the largest shard; two sets so that the gather
-    # of step k overlaps the cast of step k+1
-    n_pad = shard.max_shard_count(W, H, world) * nframes
-    nbuf = 2 if gather else 1
+    # The exchange: frame f is displayed by rank f, so every frame's tile-row shards are gathered to
+    # its own rank — one all-to-all per step (rank r sends its rows of frame f to rank f), which
+    # spreads the traffic over every rank's xGMI links instead of funnelling N frames into rank 0.
+    # Hit records travel as 12-B wire records (svo_hits_pack); the image (--shade) and AO counts as
+    # they are.
+    wire_fmt = gather and not args.shade
+    n_mine = rt.Tree.count(desc) // nframes  # my records of one frame
+    counts = [shard.shard_count(W, H, r, world) for r in range(world)]  # rank r's records of one frame
+    nbuf = 2 if gather else 1  # the exchange of step k overlaps the cast of step k+1
     gdev = torch.device("cuda", dev)
-    outs, payloads = [], []
+    outs, sends, recvs = [], [], []
     for _ in range(nbuf):
-        flat, views = shard.alloc_flat(n_pad, gdev)
-        if args.shade:  # the image is the product: gather it instead of the hit records
-            views["rgba"] = torch.zeros((n_pad, 4), dtype=torch.float32, device=gdev)
-            flat = views["rgba"].view(-1)
-        if args.ao:
-            views["ao"] = torch.zeros(n_pad, dtype=torch.uint8, device=gdev)
+        views = rt.Tree.alloc_hits(n_mine * nframes, dev, ao=args.ao > 0)
+        if args.shade:  # the image is the product: exchange it instead of the hit records
+            views["rgba"] = torch.zeros((n_mine * nframes, 4), dtype=torch.float32, device=gdev)
         outs.append(views)
-        payloads.append(torch.zeros((n_pad, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev) if wire_fmt else flat)
+        if gather:
+            snd, rcv = [], []
+            if wire_fmt:
+                snd.append(torch.zeros((n_mine * nframes, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
+                rcv.append(torch.zeros((W * H, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
+            if args.ao:
+                snd.append(views["ao"])
+                rcv.append(torch.zeros(W * H, dtype=torch.uint8, device=gdev))
+            if args.shade:
+                snd.append(views["rgba"])
+                rcv.append(torch.zeros((W * H, 4), dtype=torch.float32, device=gdev))
+            sends.append(snd)
+            recvs.append(rcv)
     stream = torch.cuda.Stream(device=dev)
-    glists, glists_host, src_descs, src_hits = None, None, None, None
-    if gather and rank == 0:
-        glists = [[torch.empty_like(payloads[0]) for _ in range(world)] for _ in range(nbuf)]
-        if args.dist_backend != "nccl":  # gloo rehearsal: gathers through host copies
-            glists_host = [[torch.empty_like(payloads[0], device="cpu") for _ in range(world)] for _ in range(nbuf)]
-        if wire_fmt:  # rank 0 unpacks every rank's records (its tile rows of every frame)
-            src_descs = [rt.Tree.frame_desc(frame_origin(0), cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world,
-                                            frame_origins=[frame_origin(f) for f in range(nframes)]) for r in range(world)]
-            src_hits = [rt.Tree.alloc_hits(n_pad, dev) for _ in range(world)]
-    pending = {}  # step -> async gather work
+    src_descs, frame_hits = None, None
+    if wire_fmt:  # my frame (rank) from every rank's rows, unpacked into one record buffer
+        src_descs = [rt.Tree.frame_desc(origins[rank], cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world)
+                     for r in range(world)]
+        frame_hits = rt.Tree.alloc_hits(W * H, dev)
+    offs = np.concatenate([[0], np.cumsum(counts)]).tolist()
+    pending = {}  # step -> (async all-to-all works, send buffers kept alive)
 
     def unpack_step(k):
-        """rank 0: wait (nccl: on the stream) for the gather of step k, then unpack every rank's records"""
-        pending.pop(k)[0].wait()
+        """wait (nccl: on the stream) for the exchange of step k, then unpack my frame's records"""
+        works, _ = pending.pop(k)
+        for w in works:
+            w.wait()
         b = k % nbuf
-        for r in range(world):
-            if glists_host is not None:
-                glists[b][r].copy_(glists_host[b][r], non_blocking=False)
-            if wire_fmt:
-                tree.unpack_hits(src_descs[r], glists[b][r], src_hits[r], stream)
+        if args.dist_backend != "nccl":  # gloo rehearsal: received on the host
+            for i, h in enumerate(recv_host[b]):
+                recvs[b][i].copy_(h)
+        if wire_fmt:
+            for r in range(world):
+                part = {key: v[offs[r]:offs[r + 1]] for key, v in frame_hits.items()}
+                tree.unpack_hits(src_descs[r], recvs[b][0][offs[r]:offs[r + 1]], part, stream)
+
+    recv_host = None
+    if gather and args.dist_backend != "nccl":
+        recv_host = [[torch.empty_like(x, device="cpu") for x in rcv] for rcv in recvs]
 
     def one_step(k, events=None):
         b = k % nbuf
         with torch.cuda.stream(stream):
-            if gather and rank != 0 and (k - nbuf) in pending:
-                pending.pop(k - nbuf)[0].wait()  # the gather that read this buffer set is done
             if events is not None:
                 events[0][0].record(stream)
             if args.shade:
@@ -237,22 +252,24 @@ def main():
             if not gather:
                 return
             if wire_fmt:
-                tree.pack_hits(desc, outs[b], payloads[b], stream)
+                tree.pack_hits(desc, outs[b], sends[b][0], stream)
             # asynchronous: the next step's cast runs while RCCL moves this one over xGMI (gloo
-            # rehearsal: the same pipeline through host copies)
-            send = payloads[b] if glists_host is None and args.dist_backend == "nccl" else payloads[b].cpu()
-            recv = (glists[b] if args.dist_backend == "nccl" else glists_host[b]) if rank == 0 else None
-            pending[k] = (dist.gather(send, recv, dst=0, async_op=True), send)  # (keeps the send buffer alive)
-            if rank == 0 and (k - 1) in pending:
+            # rehearsal: the same pipeline through host copies); the unpack of step k-1 follows
+            works, keep = [], []
+            for i, (snd, rcv) in enumerate(zip(sends[b], recvs[b])):
+                src = snd if args.dist_backend == "nccl" else snd.cpu()
+                dst = rcv if args.dist_backend == "nccl" else recv_host[b][i]
+                works.append(dist.all_to_all_single(dst, src, output_split_sizes=counts, input_split_sizes=[n_mine] * world,
+                                                    async_op=True))
+                keep.append(src)
+            pending[k] = (works, keep)
+            if (k - 1) in pending:
                 unpack_step(k - 1)
 
     def drain():
         with torch.cuda.stream(stream):
             for k in sorted(pending):
-                if rank == 0:
-                    unpack_step(k)
-                else:
-                    pending.pop(k)[0].wait()
+                unpack_step(k)
 
     step_no = 0
     for _ in range(args.warmup):
@@ -295,17 +312,19 @@ def main():
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
     rays_per_launch = rt.Tree.count(descs[0])
     verified = None
-    if args.verify and rank == 0 and wire_fmt:
-        # every frame reassembled from the ranks' unpacked records == a one-GPU cast of the frame
-        verified = True
-        for f in range(nframes):
-            one = rt.decode_hits(tree.cast_frame(frame_origin(f), cam, W, H, STEPS, ppx, ppy, flags=args.cast_flags))
-            for r in range(world):
-                rows = shard.shard_pixel_rows(H, r, world)
-                n_r = len(rows) * W
-                got = rt.decode_hits({k: v[f * n_r:(f + 1) * n_r] for k, v in src_hits[r].items()})
-                idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
-                verified &= all(np.array_equal(got[k], one[k][idx]) for k in ("pos", "steps", "hit", "axis", "material", "t"))
+    if args.verify and wire_fmt:
+        # my frame reassembled from every rank's unpacked records == a one-GPU cast of it
+        torch.cuda.synchronize()
+        one = rt.decode_hits(tree.cast_frame(origins[rank], cam, W, H, STEPS, ppx, ppy, flags=args.cast_flags))
+        got = rt.decode_hits(frame_hits)
+        ok = True
+        for r in range(world):
+            rows = shard.shard_pixel_rows(H, r, world)
+            idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+            ok &= all(np.array_equal(got[key][offs[r]:offs[r + 1]], one[key][idx]) for key in ("pos", "steps", "hit", "axis", "material", "t"))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        verified = bool(flag.item())
 
     if args.stats and rank == 0:
         d0 = descs[0]
@@ -387,8 +406,9 @@ def main():
                    % (ORIGIN + CAM + (STEPS,)),
                    "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
                    "launches_per_step": 1, "gather": gather,
-                   "gather_payload": ("12-B wire hit records (svo_hits_pack), unpacked on rank 0" if wire_fmt else
-                                      ("rgba image" if args.shade else "24-B hit records + AO counts")) if gather else None, "tree_nodes": info.n_nodes,
+                   "exchange": ("frame f gathered to rank f (one all-to-all per step, overlapped with the next cast): " +
+                                ("rgba image" if args.shade else "12-B wire hit records (svo_hits_pack), unpacked on arrival" +
+                                 (" + AO counts" if args.ao else ""))) if gather else None, "tree_nodes": info.n_nodes,
                    "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
                    "tree_builder": "host" if args.host_build else "gpu"},
         "roofline": roof,

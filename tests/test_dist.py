@@ -77,7 +77,7 @@ def test_tile_row_shard_gather_reassemble(world):
         assert np.array_equal(full[k], want[k].numpy()), k
 
 
-def _wire_worker(rank, world, port, W, H, origins, q):
+def _wire_worker(rank, world, port, W, H, origins, q, all_to_all=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
@@ -100,14 +100,61 @@ def _wire_worker(rank, world, port, W, H, origins, q):
         r = _records(ref, np.arange(len(pix)))
         cell = np.trunc(np.asarray(org, np.float32)).astype(np.int32)
         parts.append(wire_ref.pack(r["pos_steps"].numpy(), r["t"].numpy(), r["info"].numpy().view(np.uint32), cell[None, :]))
-    n_pad = shard.max_shard_count(W, H, world) * len(origins)
-    wire = torch.zeros((n_pad, 12), dtype=torch.uint8)
     mine = np.concatenate(parts)
-    wire[: len(mine)] = torch.from_numpy(mine)
-    got = shard.gather_to_root(wire, rank, world)
-    if rank == 0:
-        q.put([g.numpy().copy() for g in got])
+    if all_to_all:
+        # frame f displayed by rank f (frames = ranks): my rows of frame f go to rank f
+        counts = [shard.shard_count(W, H, r, world) for r in range(world)]
+        recv = torch.zeros((W * H, 12), dtype=torch.uint8)
+        dist.all_to_all_single(recv, torch.from_numpy(mine), output_split_sizes=counts, input_split_sizes=[len(pix)] * world)
+        q.put((rank, recv.numpy().copy()))
+    else:
+        n_pad = shard.max_shard_count(W, H, world) * len(origins)
+        wire = torch.zeros((n_pad, 12), dtype=torch.uint8)
+        wire[: len(mine)] = torch.from_numpy(mine)
+        got = shard.gather_to_root(wire, rank, world)
+        if rank == 0:
+            q.put([g.numpy().copy() for g in got])
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wire_all_to_all_frame_per_rank(world):
+    """bench.py's N>1 exchange: N frames per step, frame f displayed by rank f — one all-to-all of
+    12-B wire records; every rank's frame, unpacked, equals its single-rank cast."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wire_ref
+    from oracle import oracle as O
+    from raytracing_test_amd import shard
+
+    W, H = 64, 44
+    origins = [(4.0 + 64.0 * f, 90.0, 4.0 + 64.0 * f) for f in range(world)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_wire_worker, args=(r, world, port, W, H, origins, q, True)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(world))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    T = O.Tree.reference_world()
+    cam = O.normalize([1, -0.45, 1])
+    counts = [shard.shard_count(W, H, r, world) for r in range(world)]
+    offs = np.concatenate([[0], np.cumsum(counts)])
+    for f, org in enumerate(origins):
+        want = _records(T.cast_frame(org, cam, W, H, 300), np.arange(W * H))
+        cell = np.trunc(np.asarray(org, np.float32)).astype(np.int32)[None, :]
+        for r in range(world):
+            rows = shard.shard_pixel_rows(H, r, world)
+            idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
+            ps_, t_, info_ = wire_ref.unpack(got[f][offs[r]:offs[r + 1]], cell, 300)
+            assert np.array_equal(ps_, want["pos_steps"].numpy()[idx]), (f, r)
+            assert np.array_equal(t_, want["t"].numpy()[idx]), (f, r)
+            assert np.array_equal(info_.view(np.int32), want["info"].numpy()[idx]), (f, r)
 
 
 @pytest.mark.parametrize("world", [2, 3])
