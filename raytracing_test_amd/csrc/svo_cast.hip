@@ -248,7 +248,8 @@ __device__ __forceinline__ uint32_t nonzero16(uint32_t v) {
 
 // Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
 // the run along x from the mask row, then whole rows along z, then whole planes along y), all from
-// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
+// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it,
+// less one (the index of the step that leaves).
 __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, const uint32_t ud[3],
                                           int32_t e[3]) {
     const uint32_t cx = __builtin_amdgcn_ubfe(w[0], sh, 2u), cy = __builtin_amdgcn_ubfe(w[1], sh, 2u), cz = __builtin_amdgcn_ubfe(w[2], sh, 2u);
@@ -273,11 +274,12 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     const uint32_t nb = (((q & 0x7777u) + 0x7777u) | q) & 0x8888u;
     run_fwd(__builtin_amdgcn_ubfe(__umul24(nb, 0x249u), 12u, 4u), cy, py, ud[1], ty, ym);
     (void)ym;
-    // steps to leave: t cells of 2^sh voxels, less the part of the current cell behind the ray
+    // steps to leave: t cells of 2^sh voxels, less the part of the current cell behind the ray;
+    // less one: x + ~y = x - y - 1
     const uint32_t m = (1u << sh) - 1u;
-    e[0] = (int32_t)((tx << sh) - ((px ? w[0] : ~w[0]) & m));
-    e[1] = (int32_t)((ty << sh) - ((py ? w[1] : ~w[1]) & m));
-    e[2] = (int32_t)((tz << sh) - ((pz ? w[2] : ~w[2]) & m));
+    e[0] = (int32_t)((tx << sh) + ~((px ? w[0] : ~w[0]) & m));
+    e[1] = (int32_t)((ty << sh) + ~((py ? w[1] : ~w[1]) & m));
+    e[2] = (int32_t)((tz << sh) + ~((pz ? w[2] : ~w[2]) & m));
 }
 #else
 // Free slots of a 4-slot line (bit = occupied) beyond slot c in the step direction, before an
@@ -305,7 +307,8 @@ __device__ __forceinline__ uint32_t run_bits(uint32_t c, uint32_t n, bool pos) {
 
 // Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
 // the run along x from the mask row, then whole rows along z, then whole planes along y), all from
-// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it.
+// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it,
+// less one (the index of the step that leaves).
 __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, const uint32_t*,
                                           int32_t e[3]) {
     const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
@@ -335,9 +338,9 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     const uint32_t ny = run_fwd(yocc, cy, py);
     // steps to leave: the n further cells, plus the steps to leave the current cell
     const uint32_t m = (1u << sh) - 1u;
-    e[0] = (int32_t)((nx << sh) + ((px ? ~w[0] : w[0]) & m) + 1u);
-    e[1] = (int32_t)((ny << sh) + ((py ? ~w[1] : w[1]) & m) + 1u);
-    e[2] = (int32_t)((nz << sh) + ((pz ? ~w[2] : w[2]) & m) + 1u);
+    e[0] = (int32_t)((nx << sh) + ((px ? ~w[0] : w[0]) & m));
+    e[1] = (int32_t)((ny << sh) + ((py ? ~w[1] : w[1]) & m));
+    e[2] = (int32_t)((nz << sh) + ((pz ? ~w[2] : w[2]) & m));
 }
 #endif
 
@@ -353,13 +356,13 @@ __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, do
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
 // leave the box.  Returns false (state unchanged) when the budget ends inside the box.
 __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
-    const int32_t lim = R.steps + 1;  // exits beyond the budget are clamped (safe: total > steps)
+    // ex = steps to leave, less one; exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
     double E[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        e[k] = min(ex[k], lim);
-        E[k] = on_grid(R.T[k], e[k] - 1, R.a(k));
+        e[k] = min(ex[k], R.steps);
+        E[k] = on_grid(R.T[k], e[k], R.a(k));
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
