@@ -91,6 +91,9 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #ifndef SVO_FMA
 #define SVO_FMA 1
 #endif
+#ifndef SVO_CVT_SAT
+#define SVO_CVT_SAT 1  // crossing-count estimates through the saturating f32 -> u32 conversion
+#endif
 #ifndef SVO_P3_TLSTEP
 #define SVO_P3_TLSTEP 0  // A/B: brick walks keep the crossing value every step (one copy of the loop)
 #endif
@@ -349,7 +352,14 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 // 1/4 of the truth for counts below 2^20 (relative error < 2^-22), so m = floor(q + 1/2), clamped
 // at 0, is c-1 or c, and one exact test on the ray's grid decides: c = m + [T + m*a < W].
 __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, double W) {
+#if SVO_CVT_SAT
+    // v_cvt_u32_f32 clamps negative estimates (an axis whose next crossing lies beyond W) to 0
+    uint32_t mu;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf((float)(W - T), inva, 0.5f)));
+    const int32_t m = (int32_t)mu;
+#else
     const int32_t m = (int32_t)fmaxf(__builtin_fmaf((float)(W - T), inva, 0.5f), 0.0f);
+#endif
     return m + (int32_t)(on_grid(T, m, a) < W);
 }
 
