@@ -83,7 +83,7 @@ constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bou
 #define SVO_UNIFORM_DIRS 1
 #endif
 #ifndef SVO_BRICK_PACK
-#define SVO_BRICK_PACK 2  // 3: measured equal (brick_walk3), with a spill
+#define SVO_BRICK_PACK 4  // 2: the index + 64 form; 3: measured equal (brick_walk3), with a spill
 #endif
 #ifndef SVO_INV_A
 #define SVO_INV_A 1
@@ -556,7 +556,40 @@ __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[
 template <bool STATS, bool TLAST>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
-#if SVO_BRICK_PACK == 2
+#if SVO_BRICK_PACK == 4
+    // 127 - voxel index (byte 0: the 64-bit shift reads its low 6 bits, 63 - v, which moves the
+    // voxel's bit to bit 63 — one shift and a sign test; the +-1/4/16 moves of a walk stay within
+    // 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register.  The step keeps
+    // its delta instead of the axis: the axis follows from the last delta after the walk.
+    uint32_t pk = (left0 << 8) | (127u - child_slot(w[0], w[1], w[2], 0u));
+    const uint32_t d0 = (uint32_t)(-R.s[0]) - 0x100u, d1 = (uint32_t)(-R.s[1] * 4) - 0x10000u, d2 = (uint32_t)(-R.s[2] * 16) - 0x1000000u;
+    uint32_t dl = 0u;
+    bool go;
+    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
+        solid = (int64_t)(bmask << (pk & 63u)) < 0;
+        go = !solid && R.steps > 0;
+        if (go) {
+            // one DDA step (ray_caster.cpp:70-80) without position updates
+            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
+            const bool cy = !cx && (R.T[1] < R.T[2]);
+            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
+            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
+            R.T[2] = (cx || cy) ? R.T[2] : R.T[2] + R.a(2);  // (a mask or, not a fourth f64 compare)
+            R.steps--;
+            dl = cx ? d0 : (cy ? d1 : d2);
+            pk += dl;
+            if (STATS) {
+                st.brick_steps++;
+                st.wv_brick += wave_lead();
+            }
+            go = ((pk - 0x01010100u) & ~pk & 0x80808000u) == 0u;  // no steps-left byte at 0: inside
+        }
+    } while (go);
+    if (dl != 0u) R.axis = dl == d0 ? 0u : (dl == d1 ? 1u : 2u);
+    left = pk >> 8;
+    return 63u - (pk & 63u);
+#elif SVO_BRICK_PACK == 2
     // voxel index + 64 (byte 0: the 64-bit shift reads its low 6 bits, and the +-1/4/16 moves of a
     // walk stay within 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register
     uint32_t pk = (left0 << 8) | (child_slot(w[0], w[1], w[2], 0u) + 64u);
