@@ -45,8 +45,12 @@ SVO_HD uint32_t node_material(uint32_t info) { return info >> 16; }
 // child slot of wrapped voxel coordinates at bit offset `sh` (tetrahexa_tree.cpp:127-129)
 SVO_HD uint32_t child_slot(uint32_t x, uint32_t y, uint32_t z, uint32_t sh) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    // three bit-field extracts and two shift-ors (the generic form compiles to eight VALU ops)
-    return __builtin_amdgcn_ubfe(x, sh, 2u) | (__builtin_amdgcn_ubfe(y, sh, 2u) << 2) | (__builtin_amdgcn_ubfe(z, sh, 2u) << 4);
+    // three bit-field extracts and two shift-ors (v_lshl_or_b32); the or-of-shifts form compiles to
+    // two shifts and an or3
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(r) : "v"(__builtin_amdgcn_ubfe(z, sh, 2u)), "v"(__builtin_amdgcn_ubfe(y, sh, 2u)));
+    asm("v_lshl_or_b32 %0, %1, 2, %2" : "=v"(r) : "v"(r), "v"(__builtin_amdgcn_ubfe(x, sh, 2u)));
+    return r;
 #else
     return (((z >> sh) & 3u) << 4) | (((y >> sh) & 3u) << 2) | ((x >> sh) & 3u);
 #endif
