@@ -218,15 +218,21 @@ __device__ __forceinline__ int32_t step_by(int32_t r, int32_t n, int32_t s, uint
 // A run of free cells through a 4-cell line (occupancy bits 0-3; higher bits are ignored) from the
 // ray's cell c (free itself) in its step direction: t = cells in the run (>= 1), m = their slots.
 // A sentinel bit stands for the end of the line: one ctz (up) or one clz (down) finds the run.
+// ((1 << w) - 1) << o in one v_bfm_b32 (clang emits a shift, a not and a shift)
+__device__ __forceinline__ uint32_t bfm(uint32_t w, uint32_t o) {
+    uint32_t r;
+    asm("v_bfm_b32 %0, %1, %2" : "=v"(r) : "v"(w), "v"(o));
+    return r;
+}
 __device__ __forceinline__ void run_up(uint32_t occ, uint32_t c, uint32_t& t, uint32_t& m) {
     t = (uint32_t)__builtin_ctz((occ | 16u) >> c);
-    m = ((1u << t) - 1u) << c;
+    m = bfm(t, c);
 }
 __device__ __forceinline__ void run_down(uint32_t occ, uint32_t c, uint32_t& t, uint32_t& m) {
     // slots below c at bits 1..c, the sentinel at bit 0: the highest set bit is the run's first slot
     const uint32_t lo = 31u - (uint32_t)__builtin_clz(__builtin_amdgcn_ubfe((occ << 1) | 1u, 0u, c + 1u));
     t = c + 1u - lo;
-    m = ((1u << t) - 1u) << lo;
+    m = bfm(t, lo);
 }
 __device__ __forceinline__ void run_fwd(uint32_t occ, uint32_t c, bool pos, uint32_t ud, uint32_t& t, uint32_t& m) {
     if (ud == 1u) {
