@@ -480,11 +480,11 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
         // the previous voxel lies in the parent's region (every move starts inside it), so the
         // bits in which the last step changed the stepped coordinate tell whether the ray left it
         const uint32_t diff = moved;
-        if ((diff >> (par.sh + 2u)) != 0u) {
+        if (diff >= (4u << par.sh)) {  // a bit at or above the parent region's size changed
             // left the parent's region: the deepest node of the last descent whose region also
             // holds this cell (depth levels-1-floor(h/2), h = highest differing bit) becomes the
             // parent, read back from the per-lane path in LDS
-            const int32_t da = P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1);
+            const int32_t da = P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1);  // (diff != 0)
             par.mask = path.mask[da * kBlock];
             par.ref = path.ref[da * kBlock];
             par.sh = (uint32_t)(2 * (P.levels - 1 - da));
@@ -1102,7 +1102,7 @@ __device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]
 __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const uint32_t w[3],
                                                const uint32_t hw[3], int32_t dmax) {
     const uint32_t diff = ((w[0] ^ hw[0]) | (w[1] ^ hw[1]) | (w[2] ^ hw[2])) | 1u;
-    const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__clz((int)diff)) >> 1), dmax);
+    const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1), dmax);  // (diff != 0)
     uint64_t mask = path.mask[da * kBlock];
     uint32_t ref = path.ref[da * kBlock];
     uint32_t sh = (uint32_t)(2 * (P.levels - 1 - da));
