@@ -353,7 +353,6 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 }
 #endif
 
-// Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
 // #{ j >= 0 : T + j*a < W } = c, exact under exact_axis.  The f32 estimate q ~ (W-T)/a is within
 // 1/4 of the truth for counts below 2^20 (relative error < 2^-22), so m = floor(q + 1/2), clamped
 // at 0, is c-1 or c, and one exact test on the ray's grid decides: c = m + [T + m*a < W].
