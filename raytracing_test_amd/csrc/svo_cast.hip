@@ -368,6 +368,25 @@ __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, do
     return m + (int32_t)(on_grid(T, m, a) < W);
 }
 
+#ifndef SVO_SKIP_LE
+#define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
+#endif
+// #{ j >= 0 : T + j*a < V } or #{ j >= 0 : T + j*a <= V } = m + [E < V] or m + [E <= V] with
+// E = T + m*a and the estimate m = floor((V-T)/a + 1/2) (for <=, the count is floor(x) + 1 with
+// x = (V-T)/a, and m is that or one less)
+// this lane's bit of a wave mask as 0 / 1 (one v_cndmask on the mask in SGPRs)
+__device__ __forceinline__ uint32_t lane_bit(uint64_t m) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
+    return r;
+}
+__device__ __forceinline__ int32_t count_est(double T, double a, float inva, double V, double& E) {
+    uint32_t mu;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf((float)(V - T), inva, 0.5f)));
+    E = on_grid(T, (int32_t)mu, a);
+    return (int32_t)mu;
+}
+
 // Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
 // leave the box.  Returns false (state unchanged) when the budget ends inside the box.
 __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
@@ -385,6 +404,21 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     const double V = bx ? E[0] : (by ? E[1] : E[2]);
     // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
     // (rank_k > rank_b, i.e. k < b), else T + j*a <= V, which on doubles is < nextup(V).
+#if SVO_SKIP_LE
+    // strict: x only when the exit is on y or z, y only when it is on z, z never.  On the exit
+    // axis b, E = V exactly (V is its e_b-th crossing, m = e_b): there the tie term is the flag b_b
+    // itself, so x and y need no second compare of their own for it.
+    int32_t n[3];
+    double F[3];
+    n[0] = count_est(R.T[0], R.a(0), R.inv_a(0), V, F[0]);
+    n[1] = count_est(R.T[1], R.a(1), R.inv_a(1), V, F[1]);
+    n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, F[2]);
+    n[0] += (int32_t)(F[0] < V) + (int32_t)bx;
+    // (the tie flag combined on lane masks: clang otherwise turns each flag into a 0/1 value first)
+    n[1] += (int32_t)(F[1] < V) + (int32_t)lane_bit(__ballot(by) | (__ballot(bx) & __ballot(F[1] == V)));
+    n[2] += (int32_t)(F[2] <= V);
+    const int32_t total = n[0] + n[1] + n[2];
+#else
     const uint64_t vb = (uint64_t)__double_as_longlong(V);
     const double Vn = V > 0.0 ? __longlong_as_double((long long)(vb + 1u))
                               : (V < 0.0 ? __longlong_as_double((long long)(vb - 1u)) : __longlong_as_double(1ll));
@@ -396,6 +430,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
         n[k] = count_lt_w(R.T[k], R.a(k), R.inv_a(k), strict ? V : Vn);
         total += n[k];
     }
+#endif
     if (total > R.steps) return false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
