@@ -353,6 +353,10 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 }
 #endif
 
+#ifndef SVO_SKIP_LE
+#define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
+#endif
+#if !SVO_SKIP_LE
 // #{ j >= 0 : T + j*a < W } = c, exact under exact_axis.  The f32 estimate q ~ (W-T)/a is within
 // 1/4 of the truth for counts below 2^20 (relative error < 2^-22), so m = floor(q + 1/2), clamped
 // at 0, is c-1 or c, and one exact test on the ray's grid decides: c = m + [T + m*a < W].
@@ -367,10 +371,8 @@ __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, do
 #endif
     return m + (int32_t)(on_grid(T, m, a) < W);
 }
-
-#ifndef SVO_SKIP_LE
-#define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
 #endif
+
 // #{ j >= 0 : T + j*a < V } or #{ j >= 0 : T + j*a <= V } = m + [E < V] or m + [E <= V] with
 // E = T + m*a and the estimate m = floor((V-T)/a + 1/2) (for <=, the count is floor(x) + 1 with
 // x = (V-T)/a, and m is that or one less)
@@ -378,6 +380,26 @@ __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, do
 __device__ __forceinline__ uint32_t lane_bit(uint64_t m) {
     uint32_t r;
     asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
+    return r;
+}
+#ifndef SVO_SKIP_MASKS
+#define SVO_SKIP_MASKS 1  // skip_box keeps its exit flags as lane masks
+#endif
+// per-lane selects and a carry-in add on a wave mask held in SGPRs
+__device__ __forceinline__ uint32_t sel32(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ double sel64(uint64_t m, double a, double b) {
+    const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+    const uint32_t lo = sel32(m, (uint32_t)ua, (uint32_t)ub), hi = sel32(m, (uint32_t)(ua >> 32), (uint32_t)(ub >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ int32_t add_bit(int32_t x, uint64_t m) {
+    int32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(x), "s"(m));
     return r;
 }
 __device__ __forceinline__ int32_t count_est(double T, double a, float inva, double V, double& E) {
@@ -399,9 +421,16 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
         E[k] = on_grid(R.T[k], e[k], R.a(k));
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
+#if SVO_SKIP_MASKS
+    // exit flags as lane masks (SGPRs): selects and tie terms read them directly
+    const uint64_t mx = __ballot((E[0] < E[1]) && (E[0] < E[2]));
+    const uint64_t my = __ballot(E[1] < E[2]) & ~mx;
+    const double V = sel64(mx, E[0], sel64(my, E[1], E[2]));
+#else
     const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
     const bool by = !bx && (E[1] < E[2]);
     const double V = bx ? E[0] : (by ? E[1] : E[2]);
+#endif
     // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
     // (rank_k > rank_b, i.e. k < b), else T + j*a <= V, which on doubles is < nextup(V).
 #if SVO_SKIP_LE
@@ -413,10 +442,17 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     n[0] = count_est(R.T[0], R.a(0), R.inv_a(0), V, F[0]);
     n[1] = count_est(R.T[1], R.a(1), R.inv_a(1), V, F[1]);
     n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, F[2]);
+#if SVO_SKIP_MASKS
+    // (the terms of one axis are disjoint: a tie term implies F = V)
+    n[0] = add_bit(n[0], __ballot(F[0] < V) | mx);
+    n[1] = add_bit(n[1], __ballot(F[1] < V) | my | (mx & __ballot(F[1] == V)));
+    n[2] = add_bit(n[2], __ballot(F[2] <= V));
+#else
     n[0] += (int32_t)(F[0] < V) + (int32_t)bx;
     // (the tie flag combined on lane masks: clang otherwise turns each flag into a 0/1 value first)
     n[1] += (int32_t)(F[1] < V) + (int32_t)lane_bit(__ballot(by) | (__ballot(bx) & __ballot(F[1] == V)));
     n[2] += (int32_t)(F[2] <= V);
+#endif
     const int32_t total = n[0] + n[1] + n[2];
 #else
     const uint64_t vb = (uint64_t)__double_as_longlong(V);
@@ -438,7 +474,11 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
         R.r[k] += __mul24(R.s[k], n[k]);  // 24-bit multiply-add: full rate (s = +-1, |n| < 2^21)
     }
     R.tlast = (float)V;
+#if SVO_SKIP_MASKS
+    R.axis = sel32(mx, 0u, sel32(my, 1u, 2u));
+#else
     R.axis = bx ? 0u : (by ? 1u : 2u);
+#endif
     R.steps -= total;
     return true;
 }
