@@ -376,14 +376,16 @@ __device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, do
 // #{ j >= 0 : T + j*a < V } or #{ j >= 0 : T + j*a <= V } = m + [E < V] or m + [E <= V] with
 // E = T + m*a and the estimate m = floor((V-T)/a + 1/2) (for <=, the count is floor(x) + 1 with
 // x = (V-T)/a, and m is that or one less)
+#ifndef SVO_SKIP_MASKS
+#define SVO_SKIP_MASKS SVO_SKIP_LE  // skip_box keeps its exit flags as lane masks
+#endif
+#if !SVO_SKIP_MASKS
 // this lane's bit of a wave mask as 0 / 1 (one v_cndmask on the mask in SGPRs)
 __device__ __forceinline__ uint32_t lane_bit(uint64_t m) {
     uint32_t r;
     asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
     return r;
 }
-#ifndef SVO_SKIP_MASKS
-#define SVO_SKIP_MASKS 1  // skip_box keeps its exit flags as lane masks
 #endif
 // per-lane selects and a carry-in add on a wave mask held in SGPRs
 __device__ __forceinline__ uint32_t sel32(uint64_t m, uint32_t a, uint32_t b) {
