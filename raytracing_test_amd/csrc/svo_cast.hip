@@ -353,6 +353,9 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 }
 #endif
 
+#ifndef SVO_PLAIN_TAIL
+#define SVO_PLAIN_TAIL 1  // budget-end steps after the traversal loop; inexact rays walk empty bricks
+#endif
 #ifndef SVO_SKIP_LE
 #define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
 #endif
@@ -626,7 +629,7 @@ __device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) 
     w[2] = (uint32_t)R.r[2] & wm;
 }
 
-__device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[3], uint32_t sh) {
+[[maybe_unused]] __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[3], uint32_t sh) {
     return (((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2])) >> sh) == 0u;
 }
 
@@ -925,6 +928,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                        return skip_box(R, ex);
                    }())) {
             if (STATS && fast) st.skip_out++;
+#if SVO_PLAIN_TAIL
+            if (fast) {
+                done = true;  // the budget ends inside this empty box: steps after the loop
+            } else {
+                // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
+                pend = true;
+                bmask = 0ull;
+            }
+#else
             // step through the cell without lookups (budget ends inside it, or not exact)
             const uint32_t c[3] = {w[0], w[1], w[2]};
             bool left = false;
@@ -938,6 +950,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 }
             }
             done = !left;
+#endif
         } else if (STATS) {
             st.skips++;
             st.wv_skips += wave_lead();
@@ -1090,6 +1103,17 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             mat = 0u;
         }
     }
+#if SVO_PLAIN_TAIL
+    // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
+    // whose budget ends in empty space take their last steps together).  Every other way out of
+    // the loop without a hit has spent the budget.
+    if (!hit) {
+        while (R.steps > 0) {
+            dda_step(R);
+            if (STATS) st.plain_steps++;
+        }
+    }
+#endif
     if (par_out) *par_out = par;
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum

@@ -8,7 +8,7 @@ for rep in $(seq 1 ${REPS:-4}); do
 for L in "$@"; do
   n=$(basename $L .so)
   if [ "$L" = default ]; then unset SVO_LIB; else export SVO_LIB=$PWD/$L; fi
-  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 > gpurun_out/$TAG/ab_${n}_$rep.json 2>/dev/null || exit 1
+  timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 ${BENCH_ARGS:-} > gpurun_out/$TAG/ab_${n}_$rep.json 2>/dev/null || exit 1
 done
 done
 python3 - "$TAG" "$@" <<'PY'
