@@ -878,8 +878,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
 #if SVO_BRICK_PACK == 3
     const bool allfast = !REFLECT && __ballot(fast) == __builtin_amdgcn_read_exec();
 #endif
-    bool hit = false;
-    uint32_t mat = 0u;
+    // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
+    uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
     Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
@@ -913,7 +913,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
         const uint32_t kind = lookup<STATS>(P, rsrc, path, w, moved, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
-            hit = true;
             mat = binfo >> 16;
             done = true;
         } else if (kind == R_BRICK) {
@@ -981,7 +980,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 v = brick_walk3<STATS, true>(R, bmask, w, left0, left, solid, st);
 #endif
             if (solid) {
-                hit = true;
                 mat = brick_material(P, bmask, bref, binfo, v);
                 done = true;
             } else if (R.steps <= 0 && (((left - 0x111u) & ~left & 0x888u) == 0u)) {
@@ -1004,7 +1002,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             bool solid;
             v = brick_walk<STATS, true>(R, bmask, w, left0, left, solid, st);
             if (solid) {
-                hit = true;
                 mat = brick_material(P, bmask, bref, binfo, v);
                 done = true;
             } else if (R.steps <= 0 && (((left - 0x010101u) & ~left & 0x808080u) == 0u)) {
@@ -1019,7 +1016,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             for (;;) {
                 const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
                 if ((bmask >> v) & 1ull) {
-                    hit = true;
                     mat = brick_material(P, bmask, bref, binfo, v);
                     done = true;
                     break;
@@ -1038,7 +1034,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             }
 #endif
         }
-        const uint32_t mflags = REFLECT && hit ? (P.mat_flags[mat] & 7u) : 0u;
+        const uint32_t mflags = REFLECT && mat != kNoHit ? (P.mat_flags[mat] & 7u) : 0u;
         if (REFLECT && R.steps > 0 && mflags == 3u) {
             // a reflective block (flags & 7 == 3) with budget left: undo the last crossing on the
             // hit axis, mirror that axis (step and direction) and take the next DDA step from the
@@ -1055,9 +1051,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             bounce->n++;
             bounce->m *= 0.94f;
             dda_step(R);
-            hit = false;
             done = false;
-            mat = 0u;
+            mat = kNoHit;
         } else if (REFLECT && R.steps > 0 && mflags == 5u) {
             // a refractive solid (liquid is empty here, as in castRayFromCam) with budget left:
             // tint by 0.95 and pass; the first one bends the ray (refractRay, :211-240).  The
@@ -1098,11 +1093,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                        exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
             }
             dda_step(R);
-            hit = false;
             done = false;
-            mat = 0u;
+            mat = kNoHit;
         }
     }
+    const bool hit = mat != kNoHit;
 #if SVO_PLAIN_TAIL
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
     // whose budget ends in empty space take their last steps together).  Every other way out of
@@ -1149,7 +1144,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     h.t = R.tlast;
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
-    h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (mat & MAT_MASK);
+    h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (hit ? mat & MAT_MASK : 0u);
     return h;
 }
 

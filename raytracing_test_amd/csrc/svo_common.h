@@ -64,6 +64,7 @@ SVO_HD int32_t frame_wave_cols(int32_t width, int32_t lh) { return ((width + (1 
 
 // hit-record info word (see include/svo_rt.h)
 enum : uint32_t { HIT_BIT = 1u << 31, AXIS_SHIFT = 16, NEG_BIT = 1u << 18, MAT_MASK = 0xFFFFu };
+constexpr uint32_t kNoHit = 0xFFFFFFFFu;  // trace: material id while no voxel was hit
 
 // ------------------------------------------------------------------------------------------------
 // Correctly rounded f32 division / sqrt via f64 (see header note)
