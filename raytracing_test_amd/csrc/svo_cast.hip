@@ -898,7 +898,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
-    bool pend = false;  // the lookup found a brick: step through it below
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
     while (!done) {
@@ -907,6 +906,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         uint32_t w[3];
         wrap3(R, wm, w);
         uint32_t sh = 0u;
+        bool pend = false;  // the lookup found a brick: step through it below
         const uint32_t ax = R.axis;
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
@@ -958,7 +958,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         if (pend) {
             // voxel steps inside the brick, solid mask in registers.  (Postponing bricks until
             // more lanes hold one, or bounding the steps per iteration, measured slower.)
-            pend = false;
             uint32_t w[3];
             wrap3(R, wm, w);
 #if SVO_BRICK_FAST && SVO_BRICK_PACK == 3
