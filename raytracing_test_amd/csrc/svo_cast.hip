@@ -198,7 +198,14 @@ __device__ __forceinline__ void dda_step(Ray& R) {
 #endif
 // Wave-uniform step directions per axis: 1 = every active lane steps +, 2 = every one steps -,
 // 0 = mixed.  Lanes only retire while a ray runs, so flags taken at its start stay true.
+#ifndef SVO_UD_FLAGS
+#define SVO_UD_FLAGS 1  // 0: every lane takes the mixed-sign code (A/B)
+#endif
 __device__ __forceinline__ void dir_flags(const int32_t s[3], uint32_t ud[3]) {
+    if (!SVO_UD_FLAGS) {
+        ud[0] = ud[1] = ud[2] = 0u;
+        return;
+    }
     const uint64_t ex = __builtin_amdgcn_read_exec();
 #pragma unroll
     for (int k = 0; k < 3; k++) {
