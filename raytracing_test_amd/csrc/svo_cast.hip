@@ -363,6 +363,20 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
 #ifndef SVO_PLAIN_TAIL
 #define SVO_PLAIN_TAIL 1  // budget-end steps after the traversal loop; inexact rays walk empty bricks
 #endif
+#ifndef SVO_SLOT_REV
+#define SVO_SLOT_REV 1  // child occupancy and rank through the mask shifted by 63 - slot
+#endif
+// The child mask shifted so that slot sl's bit lands on bit 63 (m << (63 - sl)): its sign is the
+// occupancy, and one more shift leaves exactly the lower slots' bits, whose popcount is the
+// child's rank among its siblings.
+__device__ __forceinline__ uint64_t slot_top(uint64_t m, uint32_t sl) { return m << (sl ^ 63u); }
+// popcount(x) + acc through the accumulating v_bcnt_u32_b32 (clang adds acc separately)
+__device__ __forceinline__ uint32_t popc_add(uint64_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"((uint32_t)x), "v"(acc));
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"((uint32_t)(x >> 32)), "v"(r));
+    return r;
+}
 #ifndef SVO_SKIP_LE
 #define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
 #endif
@@ -576,13 +590,22 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             par.sh = (uint32_t)(2 * (P.levels - 1 - da));
             if (STATS) st.path_starts++;
         }
-        const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
         sh_out = par.sh;
+#if SVO_SLOT_REV
+        const uint64_t t = slot_top(par.mask, child_slot(w[0], w[1], w[2], par.sh));
+        if ((int64_t)t >= 0) {
+            if (STATS) st.cache_empty++;
+            return R_EMPTY;
+        }
+        ni = popc_add(t << 1, par.ref);
+#else
+        const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
         if (!((par.mask >> sl) & 1ull)) {
             if (STATS) st.cache_empty++;
             return R_EMPTY;
         }
         ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
+#endif
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
         if (STATS && SVO_VROOT && dd == 0) st.root_starts++;
     } else if (STATS) {
@@ -611,9 +634,15 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             par.ref = n.ref;
             par.sh = sh;
             par.valid = true;
+#if SVO_SLOT_REV
+            const uint64_t t = slot_top(n.mask, child_slot(w[0], w[1], w[2], sh));
+            const bool occ = (int64_t)t < 0;
+            ni = popc_add(t << 1, n.ref);
+#else
             const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
             const bool occ = (n.mask >> sl) & 1ull;
             ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
+#endif
             dd++;
             more = occ && dd < P.levels;
             sh_out = occ ? 0u : sh;  // (occupied at the last level only in a malformed tree: one voxel)
