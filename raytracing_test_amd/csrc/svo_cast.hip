@@ -1239,10 +1239,16 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdg
     uint64_t res = 0ull;
     bool more = true;
     while (more) {
-        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
         more = false;
+#if SVO_SLOT_REV
+        const uint64_t t = slot_top(mask, child_slot(w[0], w[1], w[2], sh));
+        if ((int64_t)t < 0) {
+            const Node n = load_node(rsrc, popc_add(t << 1, ref));
+#else
+        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
         if ((mask >> sl) & 1ull) {
             const Node n = load_node(rsrc, ref + (uint32_t)__popcll(mask & ((1ull << sl) - 1ull)));
+#endif
             const uint32_t kind = n.info & K_KIND_MASK;
             if (kind == K_INTERIOR) {
                 mask = n.mask;
