@@ -335,6 +335,27 @@ def test_depth12_sampled_parity(rt, oracle_mod, depth12):
     assert sub["hit"].mean() > 0.99  # every ray points down and lands on terrain
 
 
+@pytest.mark.parametrize("pose,steps", [(((4, 90, 4), (1, -0.45, 1)), 200), (((4, 90, 4), (1, 0.3, 1)), 37),
+                                        (((4, 90, 4), (1, 0.3, 1)), 3000), (((2000.5, 70.25, 1000.75), (-0.3, 0.2, 1)), 777)])
+def test_depth12_budget_ends_in_air(rt, oracle_mod, depth12, pose, steps):
+    """Budgets that end in empty space, far from any voxel: those lanes leave the traversal loop
+    and take their last DDA steps after it (svo_cast.hip, trace); sampled pixels against the oracle,
+    every output field, also for a fractional origin (rays that are not exact walk empty bricks)."""
+    org, d = pose
+    T = oracle_mod.Tree.terrain(6, 4096, 4096)
+    dn = rt.normalize(list(d))
+    W, H = 480, 270
+    out = rt.decode_hits(depth12.cast_frame(org, dn, W, H, steps))
+    pix = np.unique(np.random.default_rng(steps).integers(0, W * H, 3000))
+    ref = T.cast_frame(org, dn, W, H, steps, pixels=pix, nthreads=16)
+    assert ref["rc"] == 0
+    sub = {k: v[pix] for k, v in out.items()}
+    assert np.array_equal(sub["pos"], ref["pos"]) and np.array_equal(sub["steps"], ref["steps"])
+    assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
+    assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
+    assert (~sub["hit"]).mean() > 0.2  # most of these rays end their budget in the air
+
+
 def test_depth12_full_frame_properties(rt, depth12):
     """Size-independent properties at the full bench size: determinism, every hit voxel is solid
     in the tree and its predecessor is not, steps accounting."""
