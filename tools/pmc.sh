@@ -1,14 +1,14 @@
 #!/bin/bash
 # rocprofv3 PMC passes for the cast kernel (one counter group per pass, no trace domains — see
 # MI355X_MICROARCH.md §HBM / rocprofv3 PMC slots).  Writes gpurun_out/<tag>/pmc_*/ and the summary
-# profiles-ready JSON gpurun_out/<tag>/pmc_traffic.json.
+# profiles-ready JSON gpurun_out/<tag>/pmc_traffic.json.  usage: tools/pmc.sh <tag> [bench args]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${1:-pmc}
+TAG=${1:-pmc}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline"
+BENCH="python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline $*"  # extra args: another config
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
   i=$((i+1))
