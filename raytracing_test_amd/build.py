@@ -31,8 +31,8 @@ def _run(cmd):
     subprocess.check_call(cmd)
 
 
-def build(force=False, verbose=False, out=None, build_dir=None, defines=()):
-    """out / build_dir / defines: alternate variants for A/B timing (the default is the product)"""
+def build(force=False, verbose=False, out=None, build_dir=None, defines=(), flags=()):
+    """out / build_dir / defines / flags: alternate variants for A/B timing (the default is the product)"""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     OUT_ = out or OUT
     BUILD_ = build_dir or BUILD
@@ -51,7 +51,7 @@ def build(force=False, verbose=False, out=None, build_dir=None, defines=()):
         obj = os.path.join(BUILD_, s + ".o")
         if force or _newer(obj, [src] + hdrs):
             _run([hipcc, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
-                  "-Wall"] + ["-D" + d for d in defines] + ["-c", src, "-o", obj])
+                  "-Wall"] + ["-D" + d for d in defines] + list(flags) + ["-c", src, "-o", obj])
         objs.append(obj)
     if force or _newer(OUT_, objs):
         _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT_] + objs + ["-pthread"])

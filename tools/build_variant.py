@@ -15,6 +15,7 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--rev", default=None)
     ap.add_argument("-D", action="append", default=[])
+    ap.add_argument("--flag", action="append", default=[], help="extra hipcc flags, space-separated (e.g. '-mllvm -amdgpu-sched-strategy=max-ilp')")
     a = ap.parse_args()
     src_root = ROOT
     tmp = None
@@ -27,7 +28,8 @@ def main():
 
     out = os.path.join(ROOT, "variants", "libsvo_%s.so" % a.name)
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    build.build(force=True, out=out, build_dir=os.path.join(ROOT, "variants", "b_" + a.name), defines=a.D)
+    build.build(force=True, out=out, build_dir=os.path.join(ROOT, "variants", "b_" + a.name), defines=a.D,
+                flags=[f for x in a.flag for f in x.split()])
     if tmp:
         shutil.rmtree(tmp)
     print(out)
