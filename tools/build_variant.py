@@ -29,7 +29,7 @@ def main():
     out = os.path.join(ROOT, "variants", "libsvo_%s.so" % a.name)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     build.build(force=True, out=out, build_dir=os.path.join(ROOT, "variants", "b_" + a.name), defines=a.D,
-                flags=[f for x in a.flag for f in x.split()])
+                **({"flags": [f for x in a.flag for f in x.split()]} if a.flag else {}))  # (older revisions: no flags)
     if tmp:
         shutil.rmtree(tmp)
     print(out)
