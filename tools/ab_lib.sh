@@ -16,6 +16,7 @@ import json, sys, glob, statistics, os
 tag = sys.argv[1]
 for L in sys.argv[2:]:
     n = os.path.basename(L)[:-3] if L.endswith('.so') else L
-    ms = [json.load(open(f))['roofline']['avg_launch_ms'] for f in sorted(glob.glob('gpurun_out/%s/ab_%s_*.json' % (tag, n)))]
+    ds = [json.load(open(f)) for f in sorted(glob.glob('gpurun_out/%s/ab_%s_*.json' % (tag, n)))]
+    ms = [d['roofline']['avg_launch_ms'] if d.get('roofline') else d['ms_per_step'] for d in ds]  # (shaded: no roofline)
     print('lib=%-22s ms min %.4f median %.4f  (%s)' % (n, min(ms), statistics.median(ms), ' '.join('%.4f' % m for m in ms)))
 PY
