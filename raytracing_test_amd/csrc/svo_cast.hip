@@ -71,38 +71,8 @@ struct CastParams {
     int32_t look_valid, shadow_steps;
 };
 
-#ifndef SVO_BLOCK
-#define SVO_BLOCK 64
-#endif
-constexpr int kBlock = SVO_BLOCK;  // threads per block: one tile (finer tail at the end of a launch)
-constexpr int kMaxLevels = 7;        // svo_world_create / svo_build_terrain bound
-#ifndef SVO_BRICK_FAST
-#define SVO_BRICK_FAST 1
-#endif
-#ifndef SVO_UNIFORM_DIRS
-#define SVO_UNIFORM_DIRS 1
-#endif
-#ifndef SVO_BRICK_PACK
-#define SVO_BRICK_PACK 4  // 2: the index + 64 form; 3: measured equal (brick_walk3), with a spill
-#endif
-#ifndef SVO_INV_A
-#define SVO_INV_A 1
-#endif
-#ifndef SVO_FMA
-#define SVO_FMA 1
-#endif
-#ifndef SVO_CVT_SAT
-#define SVO_CVT_SAT 1  // crossing-count estimates through the saturating f32 -> u32 conversion
-#endif
-#ifndef SVO_P3_TLSTEP
-#define SVO_P3_TLSTEP 0  // A/B: brick walks keep the crossing value every step (one copy of the loop)
-#endif
-#ifndef SVO_VROOT
-#define SVO_VROOT 1  // start every ray below a virtual parent of the root (no first-lookup branch)
-#endif
-#ifndef SVO_A_F64
-#define SVO_A_F64 0  // keep absDelta in f64 registers (A/B)
-#endif
+constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -146,35 +116,19 @@ __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
 struct Ray {
     int32_t r[3];   // current voxel (unwrapped)
     double T[3];    // next crossing per axis (deltaPos)
-#if SVO_A_F64
-    double ad[3];   // absDelta
-#else
     float af[3];    // absDelta: an f32 value widened to f64 by the reference (ray_caster.cpp:35-41)
-#endif
     int32_t s[3];   // step
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
     float tlast;    // crossing value of the last step, as output (f32)
-#if SVO_INV_A
     float ia[3];    // f32 estimate of 1/absDelta (crossing counts only estimate with it)
     __device__ __forceinline__ float inv_a(int k) const { return ia[k]; }
-#else
-    __device__ __forceinline__ float inv_a(int k) const { return __builtin_amdgcn_rcpf((float)a(k)); }
-#endif
-#if SVO_A_F64
-    __device__ __forceinline__ double a(int k) const { return ad[k]; }
-#else
     __device__ __forceinline__ double a(int k) const { return (double)af[k]; }
-#endif
 };
 
 // T + k*a for a fast ray: exact (exact_axis), so one fused operation gives the same double
 __device__ __forceinline__ double on_grid(double T, int32_t k, double a) {
-#if SVO_FMA
     return __builtin_fma((double)k, a, T);
-#else
-    return T + (double)k * a;
-#endif
 }
 
 // one DDA step (ray_caster.cpp:70-80), branch-free
@@ -193,19 +147,9 @@ __device__ __forceinline__ void dda_step(Ray& R) {
     R.steps--;
 }
 
-#ifndef SVO_BOX_V2
-#define SVO_BOX_V2 1
-#endif
 // Wave-uniform step directions per axis: 1 = every active lane steps +, 2 = every one steps -,
 // 0 = mixed.  Lanes only retire while a ray runs, so flags taken at its start stay true.
-#ifndef SVO_UD_FLAGS
-#define SVO_UD_FLAGS 1  // 0: every lane takes the mixed-sign code (A/B)
-#endif
 __device__ __forceinline__ void dir_flags(const int32_t s[3], uint32_t ud[3]) {
-    if (!SVO_UD_FLAGS) {
-        ud[0] = ud[1] = ud[2] = 0u;
-        return;
-    }
     const uint64_t ex = __builtin_amdgcn_read_exec();
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -221,7 +165,6 @@ __device__ __forceinline__ int32_t step_by(int32_t r, int32_t n, int32_t s, uint
     return s > 0 ? r + n : r - n;  // (s * n as a 24-bit multiply-add became v_mad_u64_u32)
 }
 
-#if SVO_BOX_V2
 // A run of free cells through a 4-cell line (occupancy bits 0-3; higher bits are ignored) from the
 // ray's cell c (free itself) in its step direction: t = cells in the run (>= 1), m = their slots.
 // A sentinel bit stands for the end of the line: one ctz (up) or one clz (down) finds the run.
@@ -297,75 +240,7 @@ __device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3
     e[1] = (int32_t)((ty << sh) + ~((py ? w[1] : ~w[1]) & m));
     e[2] = (int32_t)((tz << sh) + ~((pz ? w[2] : ~w[2]) & m));
 }
-#else
-// Free slots of a 4-slot line (bit = occupied) beyond slot c in the step direction, before an
-// occupied slot or the end of the line.  Branch-free.
-__device__ __forceinline__ uint32_t run_up(uint32_t occ, uint32_t c) {
-    return (uint32_t)__builtin_ctz(((occ >> c) >> 1) | (8u >> c));
-}
-__device__ __forceinline__ uint32_t run_down(uint32_t occ, uint32_t c) {
-    return c - (32u - (uint32_t)__clz((int)(occ & ((1u << c) - 1u))));
-}
-// the wave's rays nearly always share their step signs: one variant on a wave-uniform branch
-__device__ __forceinline__ uint32_t run_fwd(uint32_t occ, uint32_t c, bool pos) {
-#if SVO_UNIFORM_DIRS
-    const uint64_t b = __ballot(pos);
-    if (b == __builtin_amdgcn_read_exec()) return run_up(occ, c);
-    if (b == 0ull) return run_down(occ, c);
-#endif
-    return pos ? run_up(occ, c) : run_down(occ, c);
-}
 
-// slots c .. c+n (pos) or c-n .. c of a 4-slot line
-__device__ __forceinline__ uint32_t run_bits(uint32_t c, uint32_t n, bool pos) {
-    return ((2u << n) - 1u) << (pos ? c : c - n);
-}
-
-// Grow the ray's empty child slot into the largest forward box of empty sibling slots (greedy:
-// the run along x from the mask row, then whole rows along z, then whole planes along y), all from
-// the parent's 64-bit child mask in registers, without loops.  Returns per-axis steps to leave it,
-// less one (the index of the step that leaves).
-__device__ __forceinline__ void box_exits(const uint32_t w[3], const int32_t s[3], uint32_t sh, uint64_t pmask, const uint32_t*,
-                                          int32_t e[3]) {
-    const uint32_t cx = (w[0] >> sh) & 3u, cy = (w[1] >> sh) & 3u, cz = (w[2] >> sh) & 3u;
-    const bool px = s[0] > 0, py = s[1] > 0, pz = s[2] > 0;
-    const uint32_t lo = (uint32_t)pmask, hi = (uint32_t)(pmask >> 32);
-    // x run through the row (cy, cz)
-    const uint32_t row = (uint32_t)(pmask >> (16u * cz + 4u * cy)) & 0xFu;
-    const uint32_t nx = run_fwd(row, cx, px);
-    const uint32_t xm = run_bits(cx, nx, px);
-    // rows (cy, z) over the x run: bit z of zocc = the row holds a solid slot
-    const uint32_t xm2 = (xm | (xm << 16)) << (4u * cy);
-    const uint32_t tl = lo & xm2, th = hi & xm2;
-    const uint32_t zocc = (uint32_t)((tl & 0xFFFFu) != 0u) | ((uint32_t)(tl > 0xFFFFu) << 1) |
-                          ((uint32_t)((th & 0xFFFFu) != 0u) << 2) | ((uint32_t)(th > 0xFFFFu) << 3);
-    const uint32_t nz = run_fwd(zocc, cz, pz);
-    const uint32_t zm = run_bits(cz, nz, pz);
-    // planes y over the x run x z run: bit y of yocc = the plane holds a solid slot
-    const uint32_t xr2 = xm | (xm << 4);
-    const uint32_t xrep = xr2 | (xr2 << 8);  // xm in every y nibble (shifts: v_mul_lo is quarter rate)
-    const uint32_t pl = ((zm & 1u) ? xrep : 0u) | ((zm & 2u) ? xrep << 16 : 0u);
-    const uint32_t ph = ((zm & 4u) ? xrep : 0u) | ((zm & 8u) ? xrep << 16 : 0u);
-    uint32_t q = (lo & pl) | (hi & ph);
-    q = (q | (q >> 16)) & 0xFFFFu;
-    q |= q >> 1;
-    q |= q >> 2;
-    const uint32_t yocc = (q & 1u) | ((q >> 3) & 2u) | ((q >> 6) & 4u) | ((q >> 9) & 8u);
-    const uint32_t ny = run_fwd(yocc, cy, py);
-    // steps to leave: the n further cells, plus the steps to leave the current cell
-    const uint32_t m = (1u << sh) - 1u;
-    e[0] = (int32_t)((nx << sh) + ((px ? ~w[0] : w[0]) & m));
-    e[1] = (int32_t)((ny << sh) + ((py ? ~w[1] : w[1]) & m));
-    e[2] = (int32_t)((nz << sh) + ((pz ? ~w[2] : w[2]) & m));
-}
-#endif
-
-#ifndef SVO_PLAIN_TAIL
-#define SVO_PLAIN_TAIL 1  // budget-end steps after the traversal loop; inexact rays walk empty bricks
-#endif
-#ifndef SVO_SLOT_REV
-#define SVO_SLOT_REV 1  // child occupancy and rank through the mask shifted by 63 - slot
-#endif
 // The child mask shifted so that slot sl's bit lands on bit 63 (m << (63 - sl)): its sign is the
 // occupancy, and one more shift leaves exactly the lower slots' bits, whose popcount is the
 // child's rank among its siblings.
@@ -377,40 +252,10 @@ __device__ __forceinline__ uint32_t popc_add(uint64_t x, uint32_t acc) {
     asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"((uint32_t)(x >> 32)), "v"(r));
     return r;
 }
-#ifndef SVO_SKIP_LE
-#define SVO_SKIP_LE 1  // skip_box counts with <= against V instead of < against nextup(V)
-#endif
-#if !SVO_SKIP_LE
-// #{ j >= 0 : T + j*a < W } = c, exact under exact_axis.  The f32 estimate q ~ (W-T)/a is within
-// 1/4 of the truth for counts below 2^20 (relative error < 2^-22), so m = floor(q + 1/2), clamped
-// at 0, is c-1 or c, and one exact test on the ray's grid decides: c = m + [T + m*a < W].
-__device__ __forceinline__ int32_t count_lt_w(double T, double a, float inva, double W) {
-#if SVO_CVT_SAT
-    // v_cvt_u32_f32 clamps negative estimates (an axis whose next crossing lies beyond W) to 0
-    uint32_t mu;
-    asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf((float)(W - T), inva, 0.5f)));
-    const int32_t m = (int32_t)mu;
-#else
-    const int32_t m = (int32_t)fmaxf(__builtin_fmaf((float)(W - T), inva, 0.5f), 0.0f);
-#endif
-    return m + (int32_t)(on_grid(T, m, a) < W);
-}
-#endif
 
 // #{ j >= 0 : T + j*a < V } or #{ j >= 0 : T + j*a <= V } = m + [E < V] or m + [E <= V] with
 // E = T + m*a and the estimate m = floor((V-T)/a + 1/2) (for <=, the count is floor(x) + 1 with
 // x = (V-T)/a, and m is that or one less)
-#ifndef SVO_SKIP_MASKS
-#define SVO_SKIP_MASKS SVO_SKIP_LE  // skip_box keeps its exit flags as lane masks
-#endif
-#if !SVO_SKIP_MASKS
-// this lane's bit of a wave mask as 0 / 1 (one v_cndmask on the mask in SGPRs)
-__device__ __forceinline__ uint32_t lane_bit(uint64_t m) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(r) : "s"(m));
-    return r;
-}
-#endif
 // per-lane selects and a carry-in add on a wave mask held in SGPRs
 __device__ __forceinline__ uint32_t sel32(uint64_t m, uint32_t a, uint32_t b) {
     uint32_t r;
@@ -447,19 +292,12 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
         E[k] = on_grid(R.T[k], e[k], R.a(k));
     }
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
-#if SVO_SKIP_MASKS
     // exit flags as lane masks (SGPRs): selects and tie terms read them directly
     const uint64_t mx = __ballot((E[0] < E[1]) && (E[0] < E[2]));
     const uint64_t my = __ballot(E[1] < E[2]) & ~mx;
     const double V = sel64(mx, E[0], sel64(my, E[1], E[2]));
-#else
-    const bool bx = (E[0] < E[1]) && (E[0] < E[2]);
-    const bool by = !bx && (E[1] < E[2]);
-    const double V = bx ? E[0] : (by ? E[1] : E[2]);
-#endif
     // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
     // (rank_k > rank_b, i.e. k < b), else T + j*a <= V, which on doubles is < nextup(V).
-#if SVO_SKIP_LE
     // strict: x only when the exit is on y or z, y only when it is on z, z never.  On the exit
     // axis b, E = V exactly (V is its e_b-th crossing, m = e_b): there the tie term is the flag b_b
     // itself, so x and y need no second compare of their own for it.
@@ -468,31 +306,11 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
     n[0] = count_est(R.T[0], R.a(0), R.inv_a(0), V, F[0]);
     n[1] = count_est(R.T[1], R.a(1), R.inv_a(1), V, F[1]);
     n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, F[2]);
-#if SVO_SKIP_MASKS
     // (the terms of one axis are disjoint: a tie term implies F = V)
     n[0] = add_bit(n[0], __ballot(F[0] < V) | mx);
     n[1] = add_bit(n[1], __ballot(F[1] < V) | my | (mx & __ballot(F[1] == V)));
     n[2] = add_bit(n[2], __ballot(F[2] <= V));
-#else
-    n[0] += (int32_t)(F[0] < V) + (int32_t)bx;
-    // (the tie flag combined on lane masks: clang otherwise turns each flag into a 0/1 value first)
-    n[1] += (int32_t)(F[1] < V) + (int32_t)lane_bit(__ballot(by) | (__ballot(bx) & __ballot(F[1] == V)));
-    n[2] += (int32_t)(F[2] <= V);
-#endif
     const int32_t total = n[0] + n[1] + n[2];
-#else
-    const uint64_t vb = (uint64_t)__double_as_longlong(V);
-    const double Vn = V > 0.0 ? __longlong_as_double((long long)(vb + 1u))
-                              : (V < 0.0 ? __longlong_as_double((long long)(vb - 1u)) : __longlong_as_double(1ll));
-    // every axis through the same count: the exit axis b counts to exactly e_b against nextup(V)
-    int32_t total = 0, n[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const bool strict = bx ? false : (by ? k == 0 : k != 2);
-        n[k] = count_lt_w(R.T[k], R.a(k), R.inv_a(k), strict ? V : Vn);
-        total += n[k];
-    }
-#endif
     if (total > R.steps) return false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -500,11 +318,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
         R.r[k] += __mul24(R.s[k], n[k]);  // 24-bit multiply-add: full rate (s = +-1, |n| < 2^21)
     }
     R.tlast = (float)V;
-#if SVO_SKIP_MASKS
     R.axis = sel32(mx, 0u, sel32(my, 1u, 2u));
-#else
-    R.axis = bx ? 0u : (by ? 1u : 2u);
-#endif
     R.steps -= total;
     return true;
 }
@@ -555,7 +369,6 @@ struct Parent {
     uint64_t mask;
     uint32_t ref;
     uint32_t sh;  // child shift: a child region is 2^sh voxels wide, the parent's 2^(sh+2)
-    bool valid;
 };
 
 // global node read through a buffer resource (32-bit offsets, never merged with the LDS path)
@@ -576,7 +389,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
     uint32_t ni = 0u;
     int32_t dd = 0;
     if (STATS) st.lookups++;
-    if (SVO_VROOT || par.valid) {
+    {
         // the previous voxel lies in the parent's region (every move starts inside it), so the
         // bits in which the last step changed the stepped coordinate tell whether the ray left it
         const uint32_t diff = moved;
@@ -591,25 +404,14 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             if (STATS) st.path_starts++;
         }
         sh_out = par.sh;
-#if SVO_SLOT_REV
         const uint64_t t = slot_top(par.mask, child_slot(w[0], w[1], w[2], par.sh));
         if ((int64_t)t >= 0) {
             if (STATS) st.cache_empty++;
             return R_EMPTY;
         }
         ni = popc_add(t << 1, par.ref);
-#else
-        const uint32_t sl = child_slot(w[0], w[1], w[2], par.sh);
-        if (!((par.mask >> sl) & 1ull)) {
-            if (STATS) st.cache_empty++;
-            return R_EMPTY;
-        }
-        ni = par.ref + (uint32_t)__popcll(par.mask & ((1ull << sl) - 1ull));
-#endif
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
-        if (STATS && SVO_VROOT && dd == 0) st.root_starts++;
-    } else if (STATS) {
-        st.root_starts++;
+        if (STATS && dd == 0) st.root_starts++;
     }
     // descend (one exit: no per-exit register copies)
     uint32_t res = R_EMPTY;
@@ -633,16 +435,9 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             par.mask = n.mask;
             par.ref = n.ref;
             par.sh = sh;
-            par.valid = true;
-#if SVO_SLOT_REV
             const uint64_t t = slot_top(n.mask, child_slot(w[0], w[1], w[2], sh));
             const bool occ = (int64_t)t < 0;
             ni = popc_add(t << 1, n.ref);
-#else
-            const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
-            const bool occ = (n.mask >> sl) & 1ull;
-            ni = n.ref + (uint32_t)__popcll(n.mask & ((1ull << sl) - 1ull));
-#endif
             dd++;
             more = occ && dd < P.levels;
             sh_out = occ ? 0u : sh;  // (occupied at the last level only in a malformed tree: one voxel)
@@ -665,19 +460,14 @@ __device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) 
     w[2] = (uint32_t)R.r[2] & wm;
 }
 
-[[maybe_unused]] __device__ __forceinline__ bool same_cell(const uint32_t a[3], const uint32_t b[3], uint32_t sh) {
-    return (((a[0] ^ b[0]) | (a[1] ^ b[1]) | (a[2] ^ b[2])) >> sh) == 0u;
-}
-
 // One ray with castRayFromCam semantics.
 // Voxel steps through a brick on its register mask (see trace): returns the voxel index reached;
 // `left` = per-axis steps left in the brick (bytes 0-2, a zero byte = left the brick), `solid` =
-// stopped on a solid voxel.  TLAST: keep the crossing value of every step.  (Recovering it after the
-// walk as T - a, exact for fast rays, measured no faster.)
-template <bool STATS, bool TLAST>
+// stopped on a solid voxel.  The crossing value of every step is kept (recovering it after the
+// walk as T - a, exact for fast rays, measured no faster).
+template <bool STATS>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
-#if SVO_BRICK_PACK == 4
     // 127 - voxel index (byte 0: the 64-bit shift reads its low 6 bits, 63 - v, which moves the
     // voxel's bit to bit 63 — one shift and a sign test; the +-1/4/16 moves of a walk stay within
     // 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register.  The step keeps
@@ -693,7 +483,7 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
             // one DDA step (ray_caster.cpp:70-80) without position updates
             const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
             const bool cy = !cx && (R.T[1] < R.T[2]);
-            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
             R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
             R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
             R.T[2] = (cx || cy) ? R.T[2] : R.T[2] + R.a(2);  // (a mask or, not a fourth f64 compare)
@@ -710,145 +500,6 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
     if (dl != 0u) R.axis = dl == d0 ? 0u : (dl == d1 ? 1u : 2u);
     left = pk >> 8;
     return 63u - (pk & 63u);
-#elif SVO_BRICK_PACK == 2
-    // voxel index + 64 (byte 0: the 64-bit shift reads its low 6 bits, and the +-1/4/16 moves of a
-    // walk stay within 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register
-    uint32_t pk = (left0 << 8) | (child_slot(w[0], w[1], w[2], 0u) + 64u);
-    const uint32_t d0 = (uint32_t)R.s[0] - 0x100u, d1 = (uint32_t)(R.s[1] * 4) - 0x10000u, d2 = (uint32_t)(R.s[2] * 16) - 0x1000000u;
-    bool go;
-    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
-        solid = (bmask >> (pk & 63u)) & 1ull;
-        go = !solid && R.steps > 0;
-        if (go) {
-            // one DDA step (ray_caster.cpp:70-80) without position updates
-            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
-            const bool cy = !cx && (R.T[1] < R.T[2]);
-            const bool cz = !cx && !cy;
-            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
-            R.axis = cx ? 0u : (cy ? 1u : 2u);
-            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
-            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
-            R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
-            R.steps--;
-            pk += cx ? d0 : (cy ? d1 : d2);
-            if (STATS) {
-                st.brick_steps++;
-                st.wv_brick += wave_lead();
-            }
-            go = ((pk - 0x01010100u) & ~pk & 0x80808000u) == 0u;  // no steps-left byte at 0: inside
-        }
-    } while (go);
-    left = pk >> 8;
-    return pk & 63u;
-#elif SVO_BRICK_PACK
-    // steps left (bytes 0-2) and voxel index (byte 3) in one register: one select + add per step
-    uint32_t pk = left0 | (child_slot(w[0], w[1], w[2], 0u) << 24);
-    const uint32_t d0 = ((uint32_t)R.s[0] << 24) - 1u, d1 = ((uint32_t)(R.s[1] * 4) << 24) - 0x100u,
-                   d2 = ((uint32_t)(R.s[2] * 16) << 24) - 0x10000u;
-    bool go;
-    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
-        solid = (bmask >> (pk >> 24)) & 1ull;
-        go = !solid && R.steps > 0;
-        if (go) {
-            // one DDA step (ray_caster.cpp:70-80) without position updates
-            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
-            const bool cy = !cx && (R.T[1] < R.T[2]);
-            const bool cz = !cx && !cy;
-            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
-            R.axis = cx ? 0u : (cy ? 1u : 2u);
-            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
-            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
-            R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
-            R.steps--;
-            pk += cx ? d0 : (cy ? d1 : d2);
-            if (STATS) {
-                st.brick_steps++;
-                st.wv_brick += wave_lead();
-            }
-            go = ((pk - 0x010101u) & ~pk & 0x808080u) == 0u;  // no byte at 0: still inside
-        }
-    } while (go);
-    left = pk & 0xFFFFFFu;
-    return pk >> 24;
-#else
-    uint32_t v = child_slot(w[0], w[1], w[2], 0u);
-    const int32_t dvx = R.s[0], dvy = R.s[1] * 4, dvz = R.s[2] * 16;
-    left = left0;
-    bool go;
-    do {  // one exit: the compiler keeps the state in place (no per-exit copies)
-        solid = (bmask >> v) & 1ull;
-        go = !solid && R.steps > 0;
-        if (go) {
-            // one DDA step (ray_caster.cpp:70-80) without position updates
-            const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
-            const bool cy = !cx && (R.T[1] < R.T[2]);
-            const bool cz = !cx && !cy;
-            if (TLAST) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
-            R.axis = cx ? 0u : (cy ? 1u : 2u);
-            R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
-            R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
-            R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
-            R.steps--;
-            v += (uint32_t)(cx ? dvx : (cy ? dvy : dvz));
-            left -= cx ? 1u : (cy ? 0x100u : 0x10000u);
-            if (STATS) {
-                st.brick_steps++;
-                st.wv_brick += wave_lead();
-            }
-            go = ((left - 0x010101u) & ~left & 0x808080u) == 0u;  // no byte at 0: still inside
-        }
-    } while (go);
-    return v;
-#endif
-}
-
-// (SVO_BRICK_PACK 3) One register holds the voxel index + 64 (bits 0-7), the steps left in the
-// brick per axis (nibbles at bits 8, 12, 16; at most 4) and the step budget min(steps, 2047) (bits
-// 20-30): one add per step updates them all and one test of the fields' guard bits ends the walk,
-// so a step carries no budget count, no axis and — when every ray of the wave is exact (TL_STEP
-// false; a wave-uniform choice between two copies of the loop) — no crossing value: the axis follows from the last step's delta, the crossing value
-// from T - absDelta on that axis (exact for such rays).  Returns the voxel index; left = the
-// per-axis nibbles.
-template <bool STATS, bool TL_STEP>
-__device__ __forceinline__ uint32_t brick_walk3(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
-                                                Stats& st) {
-    const uint32_t b0 = (uint32_t)max(0, min(R.steps, 2047));
-    uint32_t pk = (b0 << 20) | (left0 << 8) | (child_slot(w[0], w[1], w[2], 0u) + 64u);
-    const uint32_t d0 = (uint32_t)R.s[0] - 0x100100u, d1 = (uint32_t)(R.s[1] * 4) - 0x101000u, d2 = (uint32_t)(R.s[2] * 16) - 0x110000u;
-    solid = (bmask >> (pk & 63u)) & 1ull;
-    bool go = !solid && b0 > 0u;
-    uint32_t dl = 0u;
-    while (go) {  // one exit: the compiler keeps the state in place
-        // one DDA step (ray_caster.cpp:70-80) without position updates
-        const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
-        const bool cy = !cx && (R.T[1] < R.T[2]);
-        const bool cz = !cx && !cy;
-        if (TL_STEP) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
-        R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
-        R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
-        R.T[2] = cz ? R.T[2] + R.a(2) : R.T[2];
-        dl = cx ? d0 : (cy ? d1 : d2);
-        pk += dl;
-        if (STATS) {
-            st.brick_steps++;
-            st.wv_brick += wave_lead();
-        }
-        const uint32_t zf = (pk - 0x111100u) & ~pk & 0x80088800u;  // guard bits of the fields now zero
-        solid = (zf & 0x88800u) == 0u && ((bmask >> (pk & 63u)) & 1ull);  // still inside: test the voxel
-        go = zf == 0u && !solid;
-    }
-    if (dl != 0u) {
-        const bool ax0 = dl == d0, ax1 = dl == d1;
-        R.axis = ax0 ? 0u : (ax1 ? 1u : 2u);
-        if (!TL_STEP) {
-            // (selects of values: a select of array elements becomes a scratch load)
-            const double t0 = R.T[0], t1 = R.T[1], t2 = R.T[2], a0 = R.a(0), a1 = R.a(1), a2 = R.a(2);
-            R.tlast = (float)(ax0 ? t0 - a0 : (ax1 ? t1 - a1 : t2 - a2));
-        }
-    }
-    R.steps -= (int32_t)(b0 - (pk >> 20));
-    left = (pk >> 8) & 0xFFFu;
-    return pk & 63u;
 }
 
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
@@ -892,45 +543,28 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         const Dda1 ax = dda_axis(o[k], d[k]);
         R.r[k] = ax.cell;
         R.T[k] = ax.dpos;
-#if SVO_A_F64
-        R.ad[k] = ax.adelta;
-#else
         R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
-#endif
         R.s[k] = ax.step;
-#if SVO_INV_A
         R.ia[k] = __builtin_amdgcn_rcpf((float)ax.adelta);
-#endif
     }
     R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_lt_w)
+    // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_est)
     bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
                 exact_axis(R.T[2], R.a(2), budget);
     uint32_t ud[3];
     dir_flags(R.s, ud);
-    // every ray of the wave exact: brick walks recover crossing values afterwards (brick_walk3)
-#if SVO_BRICK_PACK == 3
-    const bool allfast = !REFLECT && __ballot(fast) == __builtin_amdgcn_read_exec();
-#endif
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
     Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
-#if SVO_VROOT
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
-    par.valid = true;
     par.mask = 1ull;
     par.ref = 0u;
     par.sh = 2u * (uint32_t)P.levels;
-#else
-    par.valid = false;
-    par.mask = 0ull;
-    par.ref = par.sh = 0u;
-#endif
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
     // one back-edge: every path through the body ends at the loop latch
@@ -963,7 +597,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                        return skip_box(R, ex);
                    }())) {
             if (STATS && fast) st.skip_out++;
-#if SVO_PLAIN_TAIL
             if (fast) {
                 done = true;  // the budget ends inside this empty box: steps after the loop
             } else {
@@ -971,21 +604,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                 pend = true;
                 bmask = 0ull;
             }
-#else
-            // step through the cell without lookups (budget ends inside it, or not exact)
-            const uint32_t c[3] = {w[0], w[1], w[2]};
-            bool left = false;
-            while (R.steps > 0) {
-                dda_step(R);
-                if (STATS) st.plain_steps++;
-                wrap3(R, wm, w);
-                if (!same_cell(w, c, sh)) {
-                    left = true;
-                    break;
-                }
-            }
-            done = !left;
-#endif
         } else if (STATS) {
             st.skips++;
             st.wv_skips += wave_lead();
@@ -996,37 +614,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             // more lanes hold one, or bounding the steps per iteration, measured slower.)
             uint32_t w[3];
             wrap3(R, wm, w);
-#if SVO_BRICK_FAST && SVO_BRICK_PACK == 3
-            // Voxel index v, per-axis steps left in the brick and the budget are stepped in one
-            // register; positions follow from the step counts when the brick ends.
-            const uint32_t ex = R.s[0] > 0 ? 4u - (w[0] & 3u) : (w[0] & 3u) + 1u;
-            const uint32_t ey = R.s[1] > 0 ? 4u - (w[1] & 3u) : (w[1] & 3u) + 1u;
-            const uint32_t ez = R.s[2] > 0 ? 4u - (w[2] & 3u) : (w[2] & 3u) + 1u;
-            const uint32_t left0 = ex | (ey << 4) | (ez << 8);
-            uint32_t left, v;
-            bool solid;
-#if SVO_P3_TLSTEP
-            (void)allfast;
-            v = brick_walk3<STATS, true>(R, bmask, w, left0, left, solid, st);
-#else
-            if (allfast)
-                v = brick_walk3<STATS, false>(R, bmask, w, left0, left, solid, st);
-            else
-                v = brick_walk3<STATS, true>(R, bmask, w, left0, left, solid, st);
-#endif
-            if (solid) {
-                mat = brick_material(P, bmask, bref, binfo, v);
-                done = true;
-            } else if (R.steps <= 0 && (((left - 0x111u) & ~left & 0x888u) == 0u)) {
-                done = true;  // budget ended inside the brick
-            }
-            const int32_t nx = (int32_t)((left0 & 15u) - (left & 15u));
-            const int32_t ny = (int32_t)(((left0 >> 4) & 15u) - ((left >> 4) & 15u));
-            const int32_t nz = (int32_t)((left0 >> 8) - (left >> 8));
-            R.r[0] += R.s[0] > 0 ? nx : -nx;
-            R.r[1] += R.s[1] > 0 ? ny : -ny;
-            R.r[2] += R.s[2] > 0 ? nz : -nz;
-#elif SVO_BRICK_FAST
             // Voxel index v and per-axis steps left in the brick (one byte each) are stepped
             // instead of positions; positions follow from the step counts when the brick ends.
             // Steps left: 4 - c stepping up, c + 1 stepping down (c = the cell in the brick), i.e.
@@ -1035,7 +622,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             const uint32_t left0 = (((w[0] & 3u) | ((w[1] & 3u) << 8) | ((w[2] & 3u) << 16)) ^ up3) + 0x010101u;
             uint32_t left, v;
             bool solid;
-            v = brick_walk<STATS, true>(R, bmask, w, left0, left, solid, st);
+            v = brick_walk<STATS>(R, bmask, w, left0, left, solid, st);
             if (solid) {
                 mat = brick_material(P, bmask, bref, binfo, v);
                 done = true;
@@ -1046,28 +633,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             R.r[0] = step_by(R.r[0], (int32_t)(dn & 0xFFu), R.s[0], REFLECT ? 0u : ud[0]);
             R.r[1] = step_by(R.r[1], (int32_t)((dn >> 8) & 0xFFu), R.s[1], REFLECT ? 0u : ud[1]);
             R.r[2] = step_by(R.r[2], (int32_t)(dn >> 16), R.s[2], REFLECT ? 0u : ud[2]);
-#else
-            const uint32_t c[3] = {w[0], w[1], w[2]};
-            for (;;) {
-                const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
-                if ((bmask >> v) & 1ull) {
-                    mat = brick_material(P, bmask, bref, binfo, v);
-                    done = true;
-                    break;
-                }
-                if (R.steps <= 0) {
-                    done = true;
-                    break;
-                }
-                dda_step(R);
-                if (STATS) {
-                    st.brick_steps++;
-                    st.wv_brick += wave_lead();
-                }
-                wrap3(R, wm, w);
-                if (!same_cell(w, c, 2u)) break;
-            }
-#endif
         }
         const uint32_t mflags = REFLECT && mat != kNoHit ? (P.mat_flags[mat] & 7u) : 0u;
         if (REFLECT && R.steps > 0 && mflags == 3u) {
@@ -1115,14 +680,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
                     if (s < 0) ex -= 1.0;
                     R.T[k] = ad - (ex - (double)R.r[k]) * delta;
                     R.s[k] = s;
-#if SVO_A_F64
-                    R.ad[k] = ad;
-#else
                     R.af[k] = (float)ad;
-#endif
-#if SVO_INV_A
                     R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
-#endif
                 }
                 fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && exact_axis(R.T[0], R.a(0), R.steps) &&
                        exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
@@ -1133,7 +692,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         }
     }
     const bool hit = mat != kNoHit;
-#if SVO_PLAIN_TAIL
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
     // whose budget ends in empty space take their last steps together).  Every other way out of
     // the loop without a hit has spent the budget.
@@ -1143,7 +701,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
             if (STATS) st.plain_steps++;
         }
     }
-#endif
     if (par_out) *par_out = par;
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
@@ -1240,15 +797,9 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdg
     bool more = true;
     while (more) {
         more = false;
-#if SVO_SLOT_REV
         const uint64_t t = slot_top(mask, child_slot(w[0], w[1], w[2], sh));
         if ((int64_t)t < 0) {
             const Node n = load_node(rsrc, popc_add(t << 1, ref));
-#else
-        const uint32_t sl = child_slot(w[0], w[1], w[2], sh);
-        if ((mask >> sl) & 1ull) {
-            const Node n = load_node(rsrc, ref + (uint32_t)__popcll(mask & ((1ull << sl) - 1ull)));
-#endif
             const uint32_t kind = n.info & K_KIND_MASK;
             if (kind == K_INTERIOR) {
                 mask = n.mask;
@@ -1296,13 +847,10 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __a
 }
 
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
-#ifndef SVO_MIN_WAVES
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
-#define SVO_MIN_WAVES ((AO || STATS) ? 6 : 8)
-#endif
-__global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams P) {
+__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const CastParams P) {
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(P.nodes), (short)0, (int)0x7FFFFFFF, (int)0x00020000);
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
@@ -1434,7 +982,7 @@ __global__ __launch_bounds__(kBlock, SVO_MIN_WAVES) void k_cast(const CastParams
                 const int32_t st = (h.info & NEG_BIT) ? -1 : 1;  // step on the hit axis
                 const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
                 const int32_t l[3] = {lx, ly, lz};
-                if (P.ao_plan && pfin.valid && pfin.sh < 2u * (uint32_t)P.levels && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
+                if (P.ao_plan && pfin.sh < 2u * (uint32_t)P.levels && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
                     cnt = ao_count_plan(P, rsrc, path, pfin, h, l, ax, -st);
                 } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
