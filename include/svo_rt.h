@@ -123,6 +123,9 @@ int svo_tree_palette(const svo_tree* t, uint32_t id, svo_block* out);
 int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32_t z, svo_block* out, uint32_t* material_id);
 /* batched host lookup: palette ids (0 = empty) of n positions */
 int svo_tree_get_blocks(const svo_tree* t, const int32_t* xyz, int64_t n, uint32_t* material_ids);
+/* diagnostics: index of the deepest node a lookup of each voxel reads (the brick / SOLID node holding
+   it, or the interior node whose child slot for it is empty) */
+int svo_tree_node_indices(const svo_tree* t, const int32_t* xyz, int64_t n, uint64_t* node_index);
 /* copy the host image out (for tests / serialisation); byte sizes from svo_tree_get_info */
 int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nodes_bytes, void* mats, uint64_t mats_bytes);
 /* updateSsboData analogue: (re)upload the image to HBM of `device` (with room for edit blocks) */
@@ -220,6 +223,9 @@ typedef struct {
 /* svo_cast_desc.flags, scheduling (results identical): dispatch tile rows in order of the vertical
    slope of their centre ray, shallowest first (grazing rays travel furthest over terrain) */
 #define SVO_CAST_HORIZON_FIRST 1024
+/* svo_cast_desc.flags (results identical): read nodes through 64-bit addresses even when the tree is
+   small enough for 32-bit buffer offsets (trees of more than 2^28 nodes always use them) */
+#define SVO_CAST_WIDE_ADDR 2048
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

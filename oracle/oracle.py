@@ -202,6 +202,16 @@ class Tree:
         return t
 
     @classmethod
+    def heightfield(cls, levels, hts, native=False):
+        """The same collapse builder from given column tops, hts shape (width, length)."""
+        t = cls(levels, native)
+        hg = np.ascontiguousarray(np.asarray(hts, np.int32).reshape(-1))
+        rc = t.L.orc_build_terrain_collapsed(t.h, hg, hts.shape[0], hts.shape[1])
+        if rc:
+            raise ValueError("heights out of range for levels=%d (rc=%d)" % (levels, rc))
+        return t
+
+    @classmethod
     def terrain_putblock(cls, levels, width, length, native=False):
         """Clean root + genWorld via per-voxel putBlock (no debug blocks)."""
         t = cls(levels, native)

@@ -40,6 +40,7 @@ CAST_AO_TRACE = 128  # AO: trace every AO ray instead of the per-face voxel plan
 CAST_TILE_8X8 = 256  # scheduling: one wavefront per 8x8 tile (default: 16x4 pixels of its 8-pixel tile row)
 CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel tile row
 CAST_HORIZON_FIRST = 1024  # scheduling: tile rows with the shallowest centre ray first
+CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (results identical)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
@@ -131,7 +132,7 @@ ABI_SYMBOLS = (
     "svo_proj_plane", "svo_normalize", "svo_pixel_dir", "svo_pixel_dirs", "svo_get_blocks", "svo_put_blocks",
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
-    "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack",
+    "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
 )
 
 
@@ -188,6 +189,7 @@ def lib():
     L.svo_get_blocks.argtypes = [vp, vp, C.c_int64, vp]
     L.svo_put_blocks.argtypes = [vp, vp, vp, C.c_int64, i32]
     L.svo_tree_get_blocks.argtypes = [vp, vp, C.c_int64, vp]
+    L.svo_tree_node_indices.argtypes = [vp, vp, C.c_int64, vp]
     L.svo_noise2.argtypes = [C.c_int64, vp, vp, C.c_int64, vp]
     L.svo_terrain_heights.argtypes = [i32, i32, i32, vp]
     L.svo_hemisphere.argtypes = [i32, vp]
@@ -420,6 +422,14 @@ class Tree:
         _check(lib().svo_tree_get_blocks(self._h, p.ctypes.data_as(C.c_void_p), len(p), ids.ctypes.data_as(C.c_void_p)),
                "svo_tree_get_blocks")
         return ids
+
+    def node_indices(self, points):
+        """Index of the deepest node a lookup of each voxel reads (diagnostics: svo_tree_node_indices)."""
+        p = _xyz(points)
+        out = np.zeros(len(p), np.uint64)
+        _check(lib().svo_tree_node_indices(self._h, p.ctypes.data_as(C.c_void_p), len(p), out.ctypes.data_as(C.c_void_p)),
+               "svo_tree_node_indices")
+        return out
 
     def update(self, world, points, level=None):
         """Incremental edits: patch this tree after world.put_block / delete_block at `level` on

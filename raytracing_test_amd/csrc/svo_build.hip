@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <hipcub/hipcub.hpp>
+#include <algorithm>
 #include <memory>
 #include <vector>
 
@@ -96,8 +97,8 @@ __global__ void k_pyramid(const int16_t* pmn, const int16_t* pmx, int32_t px, in
 }
 
 // one wavefront per region, lane = child slot: counts of non-empty and MIXED children
-__global__ void k_count(DevTerrain T, const Region* cur, int64_t n, int32_t cs, int k, uint32_t* nkid, uint32_t* nmix) {
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__global__ void k_count(DevTerrain T, const Region* cur, int64_t r0, int64_t n, int32_t cs, int k, uint32_t* nkid, uint32_t* nmix) {
+    const int64_t r = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t sl = threadIdx.x & 63u;
     if (r >= n) return;  // whole waves exit together (n is per wave)
     const Region R = cur[r];
@@ -111,9 +112,9 @@ __global__ void k_count(DevTerrain T, const Region* cur, int64_t n, int32_t cs, 
 }
 
 // second pass: the region's INTERIOR record, its SOLID children, the next level's MIXED regions
-__global__ void k_write(DevTerrain T, const Region* cur, int64_t n, int32_t cs, int k, const uint64_t* koff, const uint64_t* moff,
+__global__ void k_write(DevTerrain T, const Region* cur, int64_t r0, int64_t n, int32_t cs, int k, const uint64_t* koff, const uint64_t* moff,
                         uint64_t base, Node* nodes, Region* next) {
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t r = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t sl = threadIdx.x & 63u;
     if (r >= n) return;
     const Region R = cur[r];
@@ -142,8 +143,8 @@ __device__ __forceinline__ bool g_uniform(uint32_t c, uint64_t solid) {
     return __ballot(c != G_EMPTY && c != first) == 0ull;
 }
 
-__global__ void k_brick_count(DevTerrain T, const Region* cur, int64_t n, uint32_t* nmat) {
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__global__ void k_brick_count(DevTerrain T, const Region* cur, int64_t r0, int64_t n, uint32_t* nmat) {
+    const int64_t r = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t v = threadIdx.x & 63u;
     if (r >= n) return;
     const uint32_t c = g_voxel(T, cur[r], v);
@@ -152,8 +153,8 @@ __global__ void k_brick_count(DevTerrain T, const Region* cur, int64_t n, uint32
     if (v == 0) nmat[r] = uni ? 0u : (uint32_t)__popcll(solid);
 }
 
-__global__ void k_brick_write(DevTerrain T, const Region* cur, int64_t n, const uint64_t* moff, Node* nodes, uint16_t* mats) {
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__global__ void k_brick_write(DevTerrain T, const Region* cur, int64_t r0, int64_t n, const uint64_t* moff, Node* nodes, uint16_t* mats) {
+    const int64_t r = r0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
     const uint32_t v = threadIdx.x & 63u;
     if (r >= n) return;
     const Region R = cur[r];
@@ -207,6 +208,19 @@ struct Pool {
 };
 
 inline uint32_t blocks_for(int64_t threads, int bs) { return (uint32_t)((threads + bs - 1) / bs); }
+
+// A dispatch holds fewer than 2^32 work-items (the HSA packet's grid size is 32-bit): the one-wave-per-
+// region kernels run over chunks of at most 2^24 regions (2^30 work-items).
+constexpr int64_t kRegionChunk = (int64_t)1 << 24;
+template <class F>
+int for_region_chunks(int64_t n, F&& launch) {
+    for (int64_t r0 = 0; r0 < n; r0 += kRegionChunk) {
+        const int64_t m = std::min(kRegionChunk, n - r0);
+        launch(r0, dim3(blocks_for(m * 64, 256)));
+        HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+    }
+    return SVO_OK;
+}
 
 int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& pool, int32_t device, svo_tree** out) {
     const int32_t E = 1 << (2 * levels);
@@ -291,21 +305,24 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
     HIP_TRY(hipMemcpy(nodes, &empty_root, sizeof(Node), hipMemcpyHostToDevice), SVO_EDEVICE);
     for (int d = 0; d < levels && ncur > 0; d++) {
         const int32_t cs = 1 << (2 * (levels - d - 1));
-        const uint32_t grid = blocks_for(ncur * 64, 256);
         if (d == levels - 1) {
             uint32_t* nmat;
             uint64_t* moff;
             rc = pool.alloc(&nmat, ncur);
             if (!rc) rc = pool.alloc(&moff, ncur);
             if (rc) return rc;
-            hipLaunchKernelGGL(k_brick_count, dim3(grid), dim3(256), 0, nullptr, T, cur, ncur, nmat);
-            HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+            rc = for_region_chunks(ncur, [&](int64_t r0, dim3 g) {
+                hipLaunchKernelGGL(k_brick_count, g, dim3(256), 0, nullptr, T, cur, r0, ncur, nmat);
+            });
+            if (rc) return rc;
             rc = scan(nmat, moff, ncur, &n_mats, tmp);
             if (rc) return rc;
             rc = pool.alloc(&mats, n_mats + 1);
             if (rc) return rc;
-            hipLaunchKernelGGL(k_brick_write, dim3(grid), dim3(256), 0, nullptr, T, cur, ncur, moff, nodes, mats);
-            HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+            rc = for_region_chunks(ncur, [&](int64_t r0, dim3 g) {
+                hipLaunchKernelGGL(k_brick_write, g, dim3(256), 0, nullptr, T, cur, r0, ncur, moff, nodes, mats);
+            });
+            if (rc) return rc;
             t->n_bricks = (uint64_t)ncur;
             break;
         }
@@ -317,8 +334,10 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
         if (!rc) rc = pool.alloc(&moff, ncur);
         if (rc) return rc;
         // the root is a region like any other (its record may become SOLID: handled below)
-        hipLaunchKernelGGL(k_count, dim3(grid), dim3(256), 0, nullptr, T, cur, ncur, cs, levels - d - 1, nkid, nmix);
-        HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+        rc = for_region_chunks(ncur, [&](int64_t r0, dim3 g) {
+            hipLaunchKernelGGL(k_count, g, dim3(256), 0, nullptr, T, cur, r0, ncur, cs, levels - d - 1, nkid, nmix);
+        });
+        if (rc) return rc;
         rc = scan(nkid, koff, ncur, &nk, tmp);
         if (!rc) rc = scan(nmix, moff, ncur, &nm, tmp);
         if (rc) return rc;
@@ -328,8 +347,10 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
         Region* next;
         rc = pool.alloc(&next, nm);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_write, dim3(grid), dim3(256), 0, nullptr, T, cur, ncur, cs, levels - d - 1, koff, moff, used, nodes, next);
-        HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+        rc = for_region_chunks(ncur, [&](int64_t r0, dim3 g) {
+            hipLaunchKernelGGL(k_write, g, dim3(256), 0, nullptr, T, cur, r0, ncur, cs, levels - d - 1, koff, moff, used, nodes, next);
+        });
+        if (rc) return rc;
         t->nodes_per_level[d + 1] = nk;
         used += nk;
         cur = next;
@@ -339,7 +360,7 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
     for (void* x : tmp) (void)hipFree(x);
     // (the root is never uniform SOLID: the extent reaches above every column, checked above)
     // host image + adoption of the device arrays (with slack for edits)
-    const uint64_t ncap = used + used / 8 + 65536, mcap = n_mats + n_mats / 8 + 65536;
+    const uint64_t ncap = std::min<uint64_t>(used + used / 8 + 65536, 1ull << 32), mcap = std::min<uint64_t>(n_mats + n_mats / 8 + 65536, 1ull << 32);
     Node* dn;
     uint16_t* dm;
     rc = pool.alloc(&dn, ncap);

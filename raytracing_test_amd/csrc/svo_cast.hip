@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 #include <utility>
 #include <vector>
@@ -371,19 +372,44 @@ struct Parent {
     uint32_t sh;  // child shift: a child region is 2^sh voxels wide, the parent's 2^(sh+2)
 };
 
-// global node read through a buffer resource (32-bit offsets, never merged with the LDS path)
-__device__ __forceinline__ Node load_node(const __amdgpu_buffer_rsrc_t rsrc, uint32_t ni) {
-    const uint32_t off = ni << 4;
-    Node n;
-    n.mask = ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) |
-             ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0) << 32);
-    n.ref = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 8, 0, 0);
-    n.info = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 12, 0, 0);
-    return n;
-}
+// Node reads.  Trees of up to kNarrowNodes nodes (4 GiB) read through a buffer resource with 32-bit
+// byte offsets (one shift per load, and buffer loads are never merged with the LDS path); larger
+// trees — the builders accept up to 2^32 nodes, 64 GiB — through 64-bit global addresses.  The host
+// picks the instance per tree (svo_cast.hip: node_addressing), so no index can wrap or fall outside
+// the resource and read zeros (an empty node) silently.
+constexpr uint64_t kNarrowNodes = 1ull << 28;  // ni << 4 stays below 2^32
 
-template <bool STATS>
-__device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
+struct BufNodes {
+    __amdgpu_buffer_rsrc_t rsrc;
+    __device__ __forceinline__ explicit BufNodes(const Node* p)
+        : rsrc(__builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(p), (short)0, (int)0xFFFFFFFFu, (int)0x00020000)) {}
+    __device__ __forceinline__ Node load(uint32_t ni) const {
+        const uint32_t off = ni << 4;
+        Node n;
+        n.mask = ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 4, 0, 0) << 32);
+        n.ref = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 8, 0, 0);
+        n.info = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off + 12, 0, 0);
+        return n;
+    }
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct WideNodes {
+    const __attribute__((address_space(1))) u32x4* p;
+    __device__ __forceinline__ explicit WideNodes(const Node* q) : p((const __attribute__((address_space(1))) u32x4*)q) {}
+    __device__ __forceinline__ Node load(uint32_t ni) const {
+        const u32x4 v = p[ni];  // 64-bit address: base + (u64)ni * 16
+        Node n;
+        n.mask = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        n.ref = v.z;
+        n.info = v.w;
+        return n;
+    }
+};
+
+template <bool STATS, class Mem>
+__device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, const Path& path,
                                            const uint32_t w[3], uint32_t moved, Parent& par, uint32_t& sh_out, uint64_t& bmask,
                                            uint32_t& bref, uint32_t& binfo, Stats& st) {
     uint32_t ni = 0u;
@@ -421,7 +447,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const __amdgpu_b
             st.wv_descents += wave_lead();
             st.loads++;
         }
-        const Node n = load_node(rsrc, ni);
+        const Node n = mem.load(ni);
         const uint32_t kind = n.info & K_KIND_MASK;
         // (read only for BRICK / SOLID results: written on every load, so the previous values need
         // no copies around it)
@@ -533,8 +559,8 @@ __device__ __forceinline__ void refract_dir(float d[3], uint32_t ax, int32_t st_
 
 // par_out: receives the parent of the region the ray ended in (it holds the final voxel; the LDS
 // path holds its ancestors at depths 0 .. levels-1-sh/2)
-template <bool STATS, bool REFLECT = false>
-__device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const float o[3],
+template <bool STATS, bool REFLECT = false, class Mem>
+__device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr) {
     Ray R;
@@ -581,7 +607,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const __amdgpu_buffer_
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
-        const uint32_t kind = lookup<STATS>(P, rsrc, path, w, moved, par, sh, bmask, bref, binfo, st);
+        const uint32_t kind = lookup<STATS>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
@@ -786,7 +812,8 @@ __device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]
 // ------------------------------------------------------------------------------------------------
 // solid mask of the 4^3 brick holding voxel w (an empty or SOLID region of any level covers whole
 // bricks: 0 or ~0)
-__device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path, const uint32_t w[3],
+template <class Mem>
+__device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& mem, const Path& path, const uint32_t w[3],
                                                const uint32_t hw[3], int32_t dmax) {
     const uint32_t diff = ((w[0] ^ hw[0]) | (w[1] ^ hw[1]) | (w[2] ^ hw[2])) | 1u;
     const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1), dmax);  // (diff != 0)
@@ -799,7 +826,7 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdg
         more = false;
         const uint64_t t = slot_top(mask, child_slot(w[0], w[1], w[2], sh));
         if ((int64_t)t < 0) {
-            const Node n = load_node(rsrc, popc_add(t << 1, ref));
+            const Node n = mem.load(popc_add(t << 1, ref));
             const uint32_t kind = n.info & K_KIND_MASK;
             if (kind == K_INTERIOR) {
                 mask = n.mask;
@@ -814,7 +841,8 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const __amdg
     return res;
 }
 
-__device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __amdgpu_buffer_rsrc_t rsrc, const Path& path,
+template <class Mem>
+__device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem& mem, const Path& path,
                                                   const Parent& pfin, const Hit& h, const int32_t l[3], uint32_t ax, int32_t sg) {
     const uint32_t face = 2u * ax + (sg < 0 ? 1u : 0u);
     const uint32_t al = ((uint32_t)l[0] & 3u) | (((uint32_t)l[1] & 3u) << 2) | (((uint32_t)l[2] & 3u) << 4);
@@ -835,7 +863,7 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __a
         // the brick's corner voxel (wrapped); its solid mask from one lookup
         const uint32_t w[3] = {((hb[0] + (e.x & 255u) - 128u) << 2) & wm, ((hb[1] + ((e.x >> 8) & 255u) - 128u) << 2) & wm,
                                ((hb[2] + ((e.x >> 16) & 255u) - 128u) << 2) & wm};
-        uint64_t m = brick_near(P, rsrc, path, w, hw, dmax) & vm;
+        uint64_t m = brick_near(P, mem, path, w, hw, dmax) & vm;
         while (m) {  // the plan voxels of this brick that are solid: their samples hit
             const uint32_t v = (uint32_t)__builtin_ctzll(m);
             const uint2 smv = sm[__popcll(vm & ((1ull << v) - 1ull))];
@@ -846,13 +874,14 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const __a
     return (uint32_t)__popcll(hits);
 }
 
-template <bool STATS, bool STAMPS, bool AO, bool SHADE>
+// WIDE: 64-bit node addresses (trees above kNarrowNodes nodes, or SVO_CAST_WIDE_ADDR)
+template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
 __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const CastParams P) {
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(P.nodes), (short)0, (int)0x7FFFFFFF, (int)0x00020000);
+    using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
+    const Mem mem(P.nodes);
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
     if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
@@ -930,7 +959,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, 1.0f, false};
-        const Hit h = trace<false, true>(P, rsrc, path, o, d, P.steps, nullptr, &bn);
+        const Hit h = trace<false, true>(P, mem, path, o, d, P.steps, nullptr, &bn);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -961,7 +990,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                     // shadow ray towards the sun from the centre of lastPos, through empty and liquid
                     const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                          (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                    dark = (trace<false>(P, rsrc, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
+                    dark = (trace<false>(P, mem, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
                 }
             }
             if (dark) c = make_float3(col.x * 0.3f * m, col.y * 0.3f * m, col.z * 0.3f * m);
@@ -969,7 +998,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS>(P, rsrc, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS>(P, mem, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
@@ -983,14 +1012,14 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                 const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
                 const int32_t l[3] = {lx, ly, lz};
                 if (P.ao_plan && pfin.sh < 2u * (uint32_t)P.levels && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
-                    cnt = ao_count_plan(P, rsrc, path, pfin, h, l, ax, -st);
+                    cnt = ao_count_plan(P, mem, path, pfin, h, l, ax, -st);
                 } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
                 for (int32_t i = 0; i < P.ao_n; i++) {
                     const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
                     float ad[3];
                     ao_dir(hv, ax, -st, ad);
-                    const Hit a = trace<false>(P, rsrc, path, ao_o, ad, P.ao_steps);
+                    const Hit a = trace<false>(P, mem, path, ao_o, ad, P.ao_steps);
                     cnt += (a.info & HIT_BIT) ? 1u : 0u;
                 }
                 }
@@ -1104,6 +1133,16 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
     return SVO_OK;
 }
 
+// node addressing of a cast over t: 64-bit when its device allocation holds more nodes than a 32-bit
+// buffer offset reaches (or on request)
+bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap > kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
+
+template <bool STATS, bool STAMPS, bool AO, bool SHADE>
+void launch_cast(bool wide, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
+    if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true>), grid, block, 0, st, P);
+    else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false>), grid, block, 0, st, P);
+}
+
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
@@ -1158,8 +1197,9 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     int64_t per_frame = 0;
     for (int32_t r = d->tile_row_start; r < tile_rows; r += d->tile_row_step) per_frame += std::min(8, d->height - r * 8);
     P.frame_records = per_frame * d->width;
-    if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 31)
-        SVO_FAIL(SVO_EINVAL, "svo_cast_rays: frame too large (2^31 wavefronts or more)");
+    // (a dispatch holds fewer than 2^32 work-items: the HSA packet's grid size is 32-bit)
+    if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
+        SVO_FAIL(SVO_ERANGE, "svo_cast_rays: frame too large (2^26 wavefronts or more in one launch)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
     if ((d->flags & SVO_CAST_HORIZON_FIRST) && P.tile_rows_local <= kMaxOrderRows) {
         // shallowest centre ray first (a stable sort of the local rows by |dir.y| of their middle pixel)
@@ -1232,8 +1272,9 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     tree_release_device(t);
     HIP_TRY(hipSetDevice(device), SVO_EDEVICE);
     // capacity for appended edit blocks (svo_tree_update / svo_tree_sync) without reallocation
-    const uint64_t ncap = t->nodes.size() + t->nodes.size() / 8 + 65536;
-    const uint64_t mcap = t->mats.size() + t->mats.size() / 8 + 65536;
+    // (node and material indices are 32-bit: no room beyond 2^32 elements)
+    const uint64_t ncap = std::min<uint64_t>(t->nodes.size() + t->nodes.size() / 8 + 65536, 1ull << 32);
+    const uint64_t mcap = std::min<uint64_t>(t->mats.size() + t->mats.size() / 8 + 65536, 1ull << 32);
     const size_t nb = ncap * sizeof(Node), mb = mcap * sizeof(uint16_t);
     const size_t wb = 4096;
     HIP_TRY(hipMalloc(&t->d_nodes, nb), SVO_ENOMEM);
@@ -1343,8 +1384,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     if (n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
-    if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
-    hipLaunchKernelGGL((k_cast<false, false, false, true>), dim3((uint32_t)blocks), dim3(kBlock), 0, (hipStream_t)stream, P);
+    if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
+    launch_cast<false, false, false, true>(wide_nodes(t, d->flags), dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -1370,18 +1411,19 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
-    if (blocks > 0x7FFFFFFF) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
+    if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
     const dim3 grid((uint32_t)blocks), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
+    const bool wide = wide_nodes(t, d->flags);
     if (P.ao_n > 0) {
-        if (P.flags & SVO_CAST_STATS) hipLaunchKernelGGL((k_cast<true, true, true, false>), grid, block, 0, st, P);
-        else hipLaunchKernelGGL((k_cast<false, false, true, false>), grid, block, 0, st, P);
+        if (P.flags & SVO_CAST_STATS) launch_cast<true, true, true, false>(wide, grid, block, st, P);
+        else launch_cast<false, false, true, false>(wide, grid, block, st, P);
     } else if (P.flags & SVO_CAST_STATS) {
-        hipLaunchKernelGGL((k_cast<true, true, false, false>), grid, block, 0, st, P);
+        launch_cast<true, true, false, false>(wide, grid, block, st, P);
     } else if (P.flags & SVO_CAST_TIMELINE) {
-        hipLaunchKernelGGL((k_cast<false, true, false, false>), grid, block, 0, st, P);
+        launch_cast<false, true, false, false>(wide, grid, block, st, P);
     } else {
-        hipLaunchKernelGGL((k_cast<false, false, false, false>), grid, block, 0, st, P);
+        launch_cast<false, false, false, false>(wide, grid, block, st, P);
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
@@ -1410,7 +1452,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    hipLaunchKernelGGL((k_cast<false, false, false, false>), dim3(1), dim3(kBlock), 0, nullptr, P);
+    launch_cast<false, false, false, false>(wide_nodes(t, 0), dim3(1), dim3(kBlock), nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     (void)hipFree(buf);
@@ -1504,6 +1546,7 @@ int wire_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* h, co
     int64_t n = 0;
     int rc = svo_cast_count(d, &n);
     if (rc) return rc;
+    if (n >= ((int64_t)1 << 32) - 256) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": too many records for one launch");
     Q.n = n;
     Q.steps = d->steps;
     Q.explicit_mode = d->ray_dirs != nullptr;

@@ -969,6 +969,24 @@ extern "C" int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32
     return SVO_OK;
 }
 
+extern "C" int svo_tree_node_indices(const svo_tree* t, const int32_t* xyz, int64_t n, uint64_t* idx) {
+    if (!t || ((!xyz || !idx) && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_tree_node_indices: NULL argument");
+    const uint32_t mk = (1u << (2 * t->levels)) - 1u;
+    for (int64_t i = 0; i < n; i++) {
+        const uint32_t wx = (uint32_t)xyz[3 * i] & mk, wy = (uint32_t)xyz[3 * i + 1] & mk, wz = (uint32_t)xyz[3 * i + 2] & mk;
+        uint32_t ni = 0;
+        for (int d = 0; d < t->levels; d++) {
+            const Node& nd = t->nodes[ni];
+            if (node_kind(nd.info) != K_INTERIOR) break;
+            const uint32_t sl = child_slot(wx, wy, wz, (uint32_t)(2 * (t->levels - 1 - d)));
+            if (!((nd.mask >> sl) & 1ull)) break;
+            ni = nd.ref + (uint32_t)__builtin_popcountll(nd.mask & ((1ull << sl) - 1ull));
+        }
+        idx[i] = ni;
+    }
+    return SVO_OK;
+}
+
 extern "C" int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nb, void* mats, uint64_t mb) {
     if (!t) SVO_FAIL(SVO_EINVAL, "svo_tree_export: NULL tree");
     if (nodes) {

@@ -65,7 +65,8 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     W = H = 256
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST,
+                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -131,7 +132,7 @@ def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
     dirs = np.array([c[1] for c in cases], np.float32)
     for steps in sorted(set(c[2] for c in cases)):
         sel = [i for i, c in enumerate(cases) if c[2] == steps]
-        for flags in (0, rt.CAST_ITERATIVE):
+        for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR):
             out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps, flags)
             compare(rt, gtree, out, ref, "edge S=%d flags=%d" % (steps, flags))
 
@@ -363,9 +364,11 @@ def test_depth12_full_frame_properties(rt, depth12):
     a = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
     b = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
     c = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_ITERATIVE))
+    e = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_WIDE_ADDR))
     for k in a:
         assert np.array_equal(a[k], b[k]), k
         assert np.array_equal(a[k], c[k]), k
+        assert np.array_equal(a[k], e[k]), k
     rng = np.random.default_rng(9)
     idx = rng.integers(0, len(a["hit"]), 20000)
     ids = depth12.get_blocks(a["pos"][idx])
