@@ -1,0 +1,29 @@
+// svo_bridge.hpp — what the drop-in shim (svo_bridge.cpp) adds to reedthorngag/raytracing_test beside
+// the reference's own declarations, which it defines over libsvo_rt (include/svo_rt.h):
+//   RAY_CASTER::castRayFromCam(int)              src/ray_caster.hpp:14
+//   initTetraHexaTree / putBlock / getBlock /
+//   deleteBlock / traverseTree                   src/voxel_data/tetrahexa_tree.hpp:12-22
+//   genWorld()                                   src/world_gen.hpp:3
+//   updateSsboData()                             src/voxel_data/voxel_allocator.hpp:38 (its inline GL
+//                                                body is replaced by this declaration)
+// The reference types (Pos, Block, RayResult, glm::vec3 cameraPos / cameraDir) come from
+// svo_bridge_types.hpp: bridge/reference/ (the reference's headers) in the reference build; the C++
+// test program (tests/bridge/) brings its own.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include "svo_bridge_types.hpp"
+#include "svo_rt.h"
+
+void updateSsboData();
+
+// render() without GL (replaces glDrawArrays of the low_res program, src/main.cpp:105-107): one
+// castRayFromCam-semantics primary ray per pixel of the camera's width x height frame into caller-owned
+// device buffers (24 B per pixel, include/svo_rt.h svo_hits), asynchronously on `stream`
+void svoCastPrimaryRays(int32_t width, int32_t height, int32_t steps, int32_t* pos_steps, float* t, uint32_t* info, hipStream_t stream);
+// the same frame shaded (low_res.frag's colour model, svo_shade_rays): one float4 per pixel
+void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream);
+// the tree the shim keeps in HBM (for direct use of the C ABI, e.g. svo_exchange_frames)
+svo_tree* svoTree();

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SVO_RT_VERSION 2  /* 2: svo_cast_desc.n_frames / frame_origins, wire records */
+#define SVO_RT_VERSION 3  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing */
 
 enum {
     SVO_OK = 0,
@@ -249,6 +249,31 @@ int svo_sync(void* hip_stream);
 #define SVO_WIRE_BYTES 12
 int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const svo_hits* hits, void* wire, void* hip_stream);
 int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* hip_stream);
+
+/* ------------------------------------------------------------- multi-GPU frame exchange ----- */
+/* frames sharded by interleaved 8-pixel tile rows (svo_cast_desc.tile_row_start = rank,
+   tile_row_step = nranks), each frame's shards gathered over RCCL to the rank that displays it.  RCCL
+   is bound at run time (librccl.so.1; the instance already in the process, e.g. torch's, if any). */
+typedef struct svo_exchange svo_exchange;
+#define SVO_NCCL_UNIQUE_ID_BYTES 128
+/* ncclGetUniqueId: call on one rank and hand the bytes to every rank */
+int svo_nccl_unique_id(void* out);
+/* a communicator of nranks ranks (ncclCommInitRank; every rank calls it), this rank's GPU `device` */
+int svo_exchange_create(int32_t nranks, int32_t rank, const void* unique_id, int32_t device, svo_exchange** out);
+/* an exchange over a communicator the caller owns (an ncclComm_t of the same RCCL instance) */
+int svo_exchange_wrap(void* nccl_comm, int32_t device, svo_exchange** out);
+void svo_exchange_destroy(svo_exchange* x);
+int svo_exchange_info(const svo_exchange* x, int32_t* rank, int32_t* nranks);
+/* One step's exchange.  d: this rank's shard of n_frames frames (as cast into `mine`, records of frame f
+   after those of frame f-1); frame f is displayed by rank f % nranks.  Packs `mine` into 12-B wire
+   records (svo_hits_pack; AO counts alongside when d->ao_samples > 0), sends every frame's shard to its
+   display rank and receives the shards of the frames this rank displays — one RCCL group of
+   point-to-point transfers: a gather for one frame, an all-to-all for nranks frames — then unpacks them
+   into frames_out: the whole frames (width x height records each, the layout of an unsharded
+   svo_cast_rays) of frames rank, rank + nranks, ... in that order (unused on ranks that display none).
+   Asynchronous on hip_stream; `mine` must not be overwritten before the stream passes this call. */
+int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const svo_hits* mine, const svo_hits* frames_out,
+                        void* hip_stream);
 
 /* ---------------------------------------------------------------------------- shading ------- */
 /* Shading pass: low_res.frag's colour model over castRayFromCam hits, one float4

@@ -306,6 +306,68 @@ EXPORT int orc_put_block(otree* t, int x, int y, int z, uint32_t bflags, uint64_
     return -1;
 }
 
+/* deleteBlock (tetrahexa_tree.cpp:293-359): walk to the depth-`level` node (splitting any leaf met
+   above it into 64 copies, :309-333), take its block, free it and its subtree (deleteChildren +
+   freeNode, :350-351) and clear its bit in the parent's bitmap.  The reference clears that bit with
+   the int expression `1 << index` (:352): x86 masks the shift count to 5 bits and the int result is
+   sign-extended to the u64 bitmap, so for index >= 31 it flips the wrong bits (index 31: bits 31-63;
+   index 32-62: bit index-32).  ref_shift = 1 reproduces that; 0 clears bit `index` (the intended
+   meaning, which libsvo_rt implements).  Returns 0, 1 when the position was already empty, or -1
+   where the reference exit(1)s. */
+EXPORT int orc_delete_block(otree* t, int x, int y, int z, int level, int ref_shift, uint32_t* flags, uint64_t* color, float* meta) {
+    int off = (t->max_depth - 1) * 2;
+    uint32_t stack[16];
+    int depth = 0;
+    stack[0] = t->root;
+    while (depth < t->max_depth) {
+        off -= 2;
+        int idx = o_child_index(x, y, z, off);
+        onode* n = NODE(t, stack[depth]);
+        if (n->flags & 1) {
+            uint32_t lf = n->flags;
+            uint64_t lc = n->w0;
+            uint32_t lm = n->w1;
+            uint32_t arr = o_alloc_array(t);
+            memset(ARR(t, arr), 0, sizeof(oarray));
+            uint32_t kids = o_alloc_consec(t, 64);
+            for (int i = 0; i < 64; i++) {
+                ARR(t, arr)->c[i] = kids + (uint32_t)i;
+                onode* k = NODE(t, kids + (uint32_t)i);
+                k->flags = lf;
+                k->w0 = lc;
+                k->w1 = lm;
+            }
+            n = NODE(t, stack[depth]);
+            n->flags = 0;
+            n->w0 = ~0ull; /* bitmap = -1: all set */
+            n->w1 = arr;
+        } else if (!((n->w0 >> idx) & 1)) {
+            *flags = 0;
+            *color = ~0ull;
+            *meta = 0.0f;
+            return 1;
+        }
+        stack[depth + 1] = ARR(t, NODE(t, stack[depth])->w1)->c[idx];
+        depth++;
+        if (depth == level) {
+            const onode* d = NODE(t, stack[depth]);
+            *flags = d->flags;
+            *color = d->w0;
+            memcpy(meta, &d->w1, 4);
+            o_delete_children(t, stack[depth]);
+            o_free_node(t, stack[depth]);
+            onode* p = NODE(t, stack[depth - 1]);
+            if (ref_shift)
+                p->w0 ^= (uint64_t)(int64_t)(int32_t)(1u << (idx & 31));
+            else
+                p->w0 &= ~(1ull << idx);
+            return 0;
+        }
+    }
+    t->error = 1; /* "hit max depth without finding leaf node!" exit(1) */
+    return -1;
+}
+
 /* initTetraHexaTree (tetrahexa_tree.cpp:13-41), including its construction defect: the root's child
    array is taken from the NODE pool (allocConsecNodes(4) -> node index 1) but read through the
    ARRAY pool, i.e. it aliases child array #1 — the second array allocated, zeroed by that

@@ -92,6 +92,8 @@ def lib(native=False):
     L.orc_root_flags.argtypes = [vp]
     L.orc_get_block.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_float)]
     L.orc_put_block.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_uint64, C.c_float, C.c_int]
+    L.orc_delete_block.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_float)]
     L.orc_init_tetra_hexa_tree.argtypes = [vp]
     L.orc_init_clean_root.argtypes = [vp]
     L.orc_noise2.restype = C.c_double
@@ -221,6 +223,13 @@ class Tree:
 
     def put_block(self, x, y, z, flags, color, meta=0.0, level=6):
         return self.L.orc_put_block(self.h, x, y, z, flags, color, meta, level)
+
+    def delete_block(self, x, y, z, level=6, ref_shift=False):
+        """deleteBlock (tetrahexa_tree.cpp:293-359); ref_shift reproduces its int `1 << index` bitmap
+        update (x86 semantics), else the intended bit clear.  Returns (rc, (flags, color, meta))."""
+        f, c, m = C.c_uint32(), C.c_uint64(), C.c_float()
+        rc = self.L.orc_delete_block(self.h, x, y, z, level, 1 if ref_shift else 0, C.byref(f), C.byref(c), C.byref(m))
+        return rc, (f.value, c.value, m.value)
 
     def get_block(self, x, y, z):
         f, c, m = C.c_uint32(), C.c_uint64(), C.c_float()

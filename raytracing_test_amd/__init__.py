@@ -133,6 +133,8 @@ ABI_SYMBOLS = (
     "svo_tree_get_blocks", "svo_noise2", "svo_terrain_heights", "svo_hemisphere", "svo_gen_heightfield",
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
+    "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
+    "svo_exchange_frames",
 )
 
 
@@ -197,6 +199,13 @@ def lib():
     L.svo_build_heightfield.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
     L.svo_build_terrain_gpu.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
     L.svo_build_heightfield_gpu.argtypes = [i32, i32, i32, vp, i32, C.POINTER(vp)]
+    L.svo_nccl_unique_id.argtypes = [vp]
+    L.svo_exchange_create.argtypes = [i32, i32, vp, i32, C.POINTER(vp)]
+    L.svo_exchange_wrap.argtypes = [vp, i32, C.POINTER(vp)]
+    L.svo_exchange_destroy.argtypes = [vp]
+    L.svo_exchange_destroy.restype = None
+    L.svo_exchange_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32)]
+    L.svo_exchange_frames.argtypes = [vp, vp, C.POINTER(CastDesc), C.POINTER(Hits), C.POINTER(Hits), vp]
     _lib = L
     return L
 
@@ -591,6 +600,50 @@ class Tree:
         _check(lib().svo_cast_ray_from_cam(self._h, _f3(pos), _f3(cam_dir), steps, C.byref(r), C.byref(b)),
                "svo_cast_ray_from_cam")
         return (tuple(r.pos), tuple(r.last_pos), r.steps), b.astuple()
+
+
+def _hits(out):
+    if out is None:
+        return None
+    ao = out.get("ao")
+    return Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), ao.data_ptr() if ao is not None else None)
+
+
+NCCL_UNIQUE_ID_BYTES = 128
+
+
+class Exchange:
+    """Multi-GPU frame exchange over RCCL (svo_exchange_*): every frame's tile-row shards gathered to
+    the rank that displays it (frame f -> rank f % nranks)."""
+
+    @staticmethod
+    def unique_id():
+        b = (C.c_uint8 * NCCL_UNIQUE_ID_BYTES)()
+        _check(lib().svo_nccl_unique_id(b), "svo_nccl_unique_id")
+        return bytes(b)
+
+    def __init__(self, nranks, rank, uid, device):
+        h = C.c_void_p()
+        buf = (C.c_uint8 * NCCL_UNIQUE_ID_BYTES).from_buffer_copy(bytes(uid))
+        _check(lib().svo_exchange_create(nranks, rank, buf, device, C.byref(h)), "svo_exchange_create")
+        self._h = h
+        self.rank, self.nranks = rank, nranks
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.svo_exchange_destroy(self._h)
+            self._h = None
+
+    def frames(self, tree, desc, mine, frames_out, stream=None):
+        """One step's exchange of `mine` (this rank's shard of desc's frames) into frames_out (the
+        whole frames this rank displays), asynchronous on `stream`."""
+        s = getattr(stream, "cuda_stream", stream)
+        fo = _hits(frames_out)
+        _check(lib().svo_exchange_frames(self._h, tree._h, C.byref(desc), C.byref(_hits(mine)), C.byref(fo) if fo else None,
+                                         C.c_void_p(s) if s else None), "svo_exchange_frames")
 
 
 def sun_dir():

@@ -15,7 +15,7 @@ BUILD = os.path.join(HERE, "_build")
 ARCH = os.environ.get("SVO_OFFLOAD_ARCH", "gfx950")
 
 HOST_SRCS = ["svo_world.cpp"]
-HIP_SRCS = ["svo_cast.hip", "svo_build.hip"]
+HIP_SRCS = ["svo_cast.hip", "svo_build.hip", "svo_exchange.hip"]
 HEADERS = ["svo_common.h", "svo_noise.h", "svo_internal.h", "svo_hip.h"]
 
 
@@ -54,9 +54,30 @@ def build(force=False, verbose=False, out=None, build_dir=None, defines=(), flag
                   "-Wall"] + ["-D" + d for d in defines] + list(flags) + ["-c", src, "-o", obj])
         objs.append(obj)
     if force or _newer(OUT_, objs):
-        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT_] + objs + ["-pthread"])
+        _run([hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", OUT_] + objs + ["-pthread", "-ldl"])
     return OUT_
+
+
+def build_bridge_test(force=False):
+    """The drop-in shim (bridge/svo_bridge.cpp) + its C++ test program (tests/bridge/bridge_test.cpp),
+    linked against libsvo_rt.so without Python: tests/bridge/_build/bridge_test."""
+    root = os.path.dirname(HERE)
+    out_dir = os.path.join(root, "tests", "bridge", "_build")
+    out = os.path.join(out_dir, "bridge_test")
+    srcs = [os.path.join(root, "bridge", "svo_bridge.cpp"), os.path.join(root, "tests", "bridge", "bridge_test.cpp")]
+    deps = srcs + [os.path.join(root, "bridge", "svo_bridge.hpp"), os.path.join(root, "tests", "bridge", "svo_bridge_types.hpp"),
+                   os.path.join(root, "include", "svo_rt.h"), OUT]
+    if not force and not _newer(out, deps):
+        return out
+    os.makedirs(out_dir, exist_ok=True)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    _run(["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(rocm, "include"),
+          "-I" + os.path.join(root, "include"), "-I" + os.path.join(root, "bridge"), "-I" + os.path.join(root, "tests", "bridge")] + srcs +
+         ["-L" + HERE, "-lsvo_rt", "-L" + os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath,$ORIGIN/../../../raytracing_test_amd",
+          "-Wl,-rpath," + os.path.join(rocm, "lib"), "-o", out])
+    return out
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_bridge_test(force="--force" in sys.argv)

@@ -1,0 +1,161 @@
+// bridge_test.cpp — the reference application's call sequence through the drop-in shim
+// (bridge/svo_bridge.cpp) and libsvo_rt's C ABI, without Python: main.cpp:173-232 (initTetraHexaTree,
+// genWorld, updateSsboData each frame, castRayFromCam(30) for lookingAtBlock), input.cpp:135-168
+// (delete the picked block, put one at lastPos) and a frame of primary rays; then a single-rank
+// multi-GPU exchange (svo_nccl_unique_id -> svo_exchange_create -> svo_exchange_frames) of a
+// two-frame cast.  Writes one JSON object to argv[1] (stdout without it; libraries may print there);
+// tests/test_gpu_bridge.py checks it against the oracle.
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "svo_bridge.hpp"
+
+vec3 cameraPos, cameraDir, sun;
+static FILE* g_out = stdout;
+
+static vec3 normalized(float x, float y, float z) {
+    const float v[3] = {x, y, z};
+    float o[3];
+    svo_normalize(v, o);
+    return vec3{o[0], o[1], o[2]};
+}
+
+static void print_ray(const char* key, const RayResult& r, bool comma = true) {
+    fprintf(g_out, "\"%s\": [%d, %d, %d, %d, %d, %d, %d]%s\n", key, r.pos.x, r.pos.y, r.pos.z, r.lastPos.x, r.lastPos.y, r.lastPos.z, r.steps,
+           comma ? "," : "");
+}
+
+#define HIPCHK(e)                                                                 \
+    do {                                                                          \
+        hipError_t x_ = (e);                                                      \
+        if (x_ != hipSuccess) {                                                   \
+            fprintf(stderr, "%s failed: %s\n", #e, hipGetErrorString(x_));        \
+            return 2;                                                             \
+        }                                                                         \
+    } while (0)
+#define SVOCHK(e)                                                                 \
+    do {                                                                          \
+        int r_ = (e);                                                             \
+        if (r_) {                                                                 \
+            fprintf(stderr, "%s failed (%d): %s\n", #e, r_, svo_last_error());    \
+            return 3;                                                             \
+        }                                                                         \
+    } while (0)
+
+int main(int argc, char** argv) {
+    if (argc > 1 && !(g_out = fopen(argv[1], "w"))) return 4;
+    sun = normalized(2, 1, 4);  // globals.cpp:23
+    initTetraHexaTree();        // main.cpp:180-190
+    genWorld();
+    updateSsboData();           // main.cpp:212 (first frame: build + upload)
+    fprintf(g_out, "{\n");
+    cameraPos = vec3{35, 50, 35};  // globals.cpp:20-21
+    cameraDir = normalized(1, 0, 1);
+    print_ray("pick_default", RAY_CASTER::castRayFromCam(30));
+    cameraPos = vec3{4, 90, 4};
+    cameraDir = normalized(1, -0.45f, 1);
+    print_ray("pick_c1", RAY_CASTER::castRayFromCam(300));  // (a miss: steps 0)
+    cameraPos = vec3{35, 60, 35};
+    cameraDir = normalized(1, -0.6f, 1);
+    const RayResult a = RAY_CASTER::castRayFromCam(300);
+    print_ray("pick_edit", a);
+    if (!a.steps) return 5;  // input.cpp:145 deletes only on a hit
+    const Block ga = getBlock(Pos{a.pos.x, a.pos.y, a.pos.z});
+    fprintf(g_out, "\"block_c1\": [%u, %llu],\n", ga.flags, (unsigned long long)ga.color);
+    // left click (input.cpp:141-149): delete the picked block; right click (:153-158): put at lastPos
+    deleteBlock(Pos{a.pos.x, a.pos.y, a.pos.z}, 6);
+    updateSsboData();  // next frame: only the edit travels
+    const RayResult b = RAY_CASTER::castRayFromCam(300);
+    print_ray("after_delete", b);
+    putBlock(Pos{b.lastPos.x, b.lastPos.y, b.lastPos.z}, Block{0x2u, 123456789ull, 0.0f}, 6);
+    updateSsboData();
+    const RayResult c = RAY_CASTER::castRayFromCam(300);
+    print_ray("after_put", c);
+    // a 4^3 block in front of the camera and a level-4 delete (the reference's level: a 4^3 block)
+    putBlock(Pos{20, 80, 20}, Block{0x0u, 777ull, 0.0f}, 5);
+    deleteBlock(Pos{20, 80, 20}, 5);  // the reference's depth 5: one voxel of it
+    updateSsboData();
+    const Block g1 = getBlock(Pos{20, 80, 20}), g2 = getBlock(Pos{21, 80, 20});
+    fprintf(g_out, "\"level_edits\": [%llu, %llu],\n", (unsigned long long)g1.color, (unsigned long long)g2.color);
+    // one frame of primary rays (render() without glDrawArrays) from the edited world
+    const int W = 64, H = 48, N = W * H;
+    int32_t* dps;
+    float* dt;
+    uint32_t* di;
+    HIPCHK(hipMalloc(&dps, (size_t)N * 16));
+    HIPCHK(hipMalloc(&dt, (size_t)N * 4));
+    HIPCHK(hipMalloc(&di, (size_t)N * 4));
+    svoCastPrimaryRays(W, H, 300, dps, dt, di, nullptr);
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<int32_t> hps((size_t)N * 4);
+    HIPCHK(hipMemcpy(hps.data(), dps, (size_t)N * 16, hipMemcpyDeviceToHost));
+    fprintf(g_out, "\"frame\": [");
+    for (int i = 0; i < N; i++) fprintf(g_out, "%d,%d,%d,%d%s", hps[4 * i], hps[4 * i + 1], hps[4 * i + 2], hps[4 * i + 3], i + 1 < N ? "," : "");
+    fprintf(g_out, "],\n");
+    // shaded frame: runs, finite
+    float* rgba;
+    HIPCHK(hipMalloc(&rgba, (size_t)N * 16));
+    svoRenderShaded(W, H, rgba, nullptr);
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<float> img((size_t)N * 4);
+    HIPCHK(hipMemcpy(img.data(), rgba, (size_t)N * 16, hipMemcpyDeviceToHost));
+    int finite = 1;
+    for (float v : img) finite &= isfinite(v) ? 1 : 0;
+    fprintf(g_out, "\"shade_finite\": %d,\n", finite);
+    // single-rank exchange of a two-frame cast (frames 0 and 1 both displayed by rank 0)
+    uint8_t uid[SVO_NCCL_UNIQUE_ID_BYTES];
+    SVOCHK(svo_nccl_unique_id(uid));
+    svo_exchange* x = nullptr;
+    SVOCHK(svo_exchange_create(1, 0, uid, 0, &x));
+    svo_cast_desc d{};
+    const float origins[6] = {35.0f, 60.0f, 35.0f, 36.5f, 70.25f, 12.75f};
+    d.cam_dir[0] = cameraDir.x;
+    d.cam_dir[1] = cameraDir.y;
+    d.cam_dir[2] = cameraDir.z;
+    d.width = W;
+    d.height = H;
+    d.tile_row_step = 1;
+    d.steps = 300;
+    d.ao_samples = 16;
+    d.ao_steps = 5;
+    d.n_frames = 2;
+    d.frame_origins = origins;
+    SVOCHK(svo_proj_plane(W, H, &d.ppx, &d.ppy));
+    const size_t R = 2 * (size_t)N;
+    int32_t *cps, *fps;
+    float *ct, *ft;
+    uint32_t *ci, *fi;
+    uint8_t *cao, *fao;
+    HIPCHK(hipMalloc(&cps, R * 16));
+    HIPCHK(hipMalloc(&ct, R * 4));
+    HIPCHK(hipMalloc(&ci, R * 4));
+    HIPCHK(hipMalloc(&cao, R));
+    HIPCHK(hipMalloc(&fps, R * 16));
+    HIPCHK(hipMalloc(&ft, R * 4));
+    HIPCHK(hipMalloc(&fi, R * 4));
+    HIPCHK(hipMalloc(&fao, R));
+    const svo_hits mine{cps, ct, ci, cao}, frames{fps, ft, fi, fao};
+    SVOCHK(svo_cast_rays(svoTree(), &d, &mine, nullptr));
+    SVOCHK(svo_exchange_frames(x, svoTree(), &d, &mine, &frames, nullptr));
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<uint8_t> h1(R * 25), h2(R * 25);
+    HIPCHK(hipMemcpy(h1.data(), cps, R * 16, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h2.data(), fps, R * 16, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h1.data() + R * 16, ct, R * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h2.data() + R * 16, ft, R * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h1.data() + R * 20, ci, R * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h2.data() + R * 20, fi, R * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h1.data() + R * 24, cao, R, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(h2.data() + R * 24, fao, R, hipMemcpyDeviceToHost));
+    int hits = 0;
+    for (size_t i = 0; i < R; i++) hits += (h1[R * 20 + 4 * i + 3] & 0x80) ? 1 : 0;
+    fprintf(g_out, "\"exchange_equal\": %d, \"exchange_hits\": %d\n", h1 == h2 ? 1 : 0, hits);
+    fprintf(g_out, "}\n");
+    svo_exchange_destroy(x);
+    if (g_out != stdout) fclose(g_out);
+    return 0;
+}

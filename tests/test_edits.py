@@ -107,3 +107,99 @@ def test_update_errors(rt):
         tree.update(w, [[0, 0, 0]], level=9)
     with pytest.raises(RuntimeError):
         tree.sync()  # not uploaded
+
+
+def _oracle_edit_replay(oracle_mod, rng, w=None, on_edit=None):
+    """putBlock / deleteBlock sequence at levels 6 / 5 / 4 applied to the product's world and to the
+    oracle's reference-layout tree (its deleteBlock restated from tetrahexa_tree.cpp:293-359 with the
+    intended bit clear: see test_reference_delete_shift_defect).  Levels: svo_delete_block takes
+    putBlock's meaning (6 = a voxel, 5 = a 4^3 block, 4 = 16^3); the reference's deleteBlock removes the
+    node at depth `level`, one level finer (5 = a voxel, 4 = a 4^3 block), except that its only caller's
+    level 6 (input.cpp:146) splits the voxel into 64 copies and drops the first, which getBlock then
+    reads (its UB shift at the voxel depth indexes slot 0): a voxel delete as well."""
+    import raytracing_test_amd as rt
+
+    T = oracle_mod.Tree.reference_world()
+    w = rt.World.reference() if w is None else w
+    edits = []
+
+    def done(pts, lv):
+        edits.append((np.asarray(pts).reshape(-1, 3), lv))
+        if on_edit:
+            on_edit(edits[-1][0], lv)
+
+    for step in range(3):
+        carve = _random_edits(rng, 60, (30, 20, 30), (120, 50, 120))
+        for p in carve:
+            x, y, z = (int(v) for v in p)
+            w.delete_block(x, y, z)
+            assert T.delete_block(x, y, z)[0] in (0, 1)
+        sky = _random_edits(rng, 40, (20, 50, 20), (150, 90, 150))
+        flags = rng.choice([0, REFLECTIVE, LIQUID | REFRACTIVE], size=len(sky)).astype(np.uint32)
+        colors = rng.integers(1, 1 << 60, len(sky)).astype(np.uint64)
+        w.put_blocks(sky, flags, colors)
+        for p, f, c in zip(sky, flags, colors):
+            assert T.put_block(int(p[0]), int(p[1]), int(p[2]), int(f), int(c), 0.0, 6) == 0
+        blk = np.array([[60 + 8 * step, 40, 60]])
+        w.put_blocks(blk, np.zeros(1, np.uint32), np.full(1, 4242, np.uint64), level=5)
+        assert T.put_block(60 + 8 * step, 40, 60, 0, 4242, 0.0, 5) == 0
+        done(carve, 6)
+        done(sky, 6)
+        done(blk, 5)
+    # level-5 and level-4 deletes (a 4^3 and a 16^3 region of terrain)
+    for (x, y, z), lv in (((88, 24, 88), 5), ((96, 16, 32), 4), ((41, 22, 37), 6)):
+        w.delete_block(x, y, z, level=lv)
+        assert T.delete_block(x, y, z, level=lv - 1)[0] in (0, 1)
+        done([[x, y, z]], lv)
+    return w, T, edits
+
+
+def test_world_edits_match_oracle(rt, oracle_mod):
+    """the product's host world (putBlock / deleteBlock) and its patched linear tree vs the oracle's
+    restatement after the same edit sequence: every probed block equal"""
+    rng = np.random.default_rng(17)
+    w, T, edits = _oracle_edit_replay(oracle_mod, rng)
+    pts = _probe_points(rng, np.concatenate([e for e, _ in edits]), 256, n_random=6000)
+    pts = pts[(pts >= 0).all(1) & (pts < 700).all(1)]  # parity domain: outside root child 63 (SURVEY.md §0.2)
+    f, c, _ = w.get_blocks(pts)
+    want = np.array([T.get_block(*[int(v) for v in p])[:2] for p in pts], dtype=object)
+    empty = 0xFFFFFFFFFFFFFFFF
+    for i, p in enumerate(pts):
+        of, oc = want[i]
+        if oc == empty:
+            assert c[i] == empty, (p, f[i], c[i])
+        else:
+            assert (f[i], c[i]) == (of, oc), (p, (f[i], c[i]), (of, oc))
+
+
+def test_reference_delete_shift_defect(oracle_mod):
+    """deleteBlock's `bitmap ^= 1 << index` (tetrahexa_tree.cpp:352) is an int shift: for child index
+    < 31 it clears the right bit, as libsvo_rt's deleteBlock does; for index >= 31 the reference flips
+    other bits (x86: count masked to 5 bits, result sign-extended) — the voxel stays, a sibling goes.
+    libsvo_rt implements the intended clear (include/svo_rt.h); this pins the divergence."""
+    def fresh():
+        T = oracle_mod.Tree(5)
+        oracle_mod.lib().orc_init_clean_root(T.h)
+        for x in range(4):
+            for z in range(4):
+                T.put_block(x, 0, z, 0, 7, 0.0, 6)
+        return T
+    # deleteBlock(p, 5): the voxel node, bit = its slot z<<4 | y<<2 | x.  (1, 0, 1): slot 17 < 31, the
+    # reference and the intended clear agree
+    for ref_shift in (False, True):
+        T = fresh()
+        assert T.delete_block(1, 0, 1, level=5, ref_shift=ref_shift)[0] == 0
+        assert T.get_block(1, 0, 1)[1] == 0xFFFFFFFFFFFFFFFF
+        assert T.get_block(2, 0, 1)[1] == 7
+    # (0, 0, 2): slot 32 -> the reference flips bit 0 instead: (0, 0, 2) stays, (0, 0, 0) vanishes
+    T = fresh()
+    T.delete_block(0, 0, 2, level=5, ref_shift=True)
+    assert T.get_block(0, 0, 2)[1] == 7 and T.get_block(0, 0, 0)[1] == 0xFFFFFFFFFFFFFFFF
+    T = fresh()
+    T.delete_block(0, 0, 2, level=5, ref_shift=False)
+    assert T.get_block(0, 0, 2)[1] == 0xFFFFFFFFFFFFFFFF and T.get_block(0, 0, 0)[1] == 7
+    # the caller's level 6 (input.cpp:146) deletes the voxel through the slot-0 accident, any slot
+    for ref_shift in (False, True):
+        T = fresh()
+        T.delete_block(0, 0, 2, level=6, ref_shift=ref_shift)
+        assert T.get_block(0, 0, 2)[1] == 0xFFFFFFFFFFFFFFFF and T.get_block(0, 0, 0)[1] == 7

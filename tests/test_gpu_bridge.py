@@ -1,0 +1,72 @@
+"""The drop-in shim from C++: tests/bridge/bridge_test (built by build.py from bridge/svo_bridge.cpp,
+linked against libsvo_rt.so, no Python in the process) runs the reference application's call sequence
+— initTetraHexaTree, genWorld, updateSsboData, RAY_CASTER::castRayFromCam, deleteBlock / putBlock
+(input.cpp:135-168), a primary-ray frame, a shaded frame — and a single-rank RCCL exchange
+(svo_exchange_frames).  Its outputs are checked here against the oracle after the same edits."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "bridge", "_build", "bridge_test")
+
+
+@pytest.fixture(scope="module")
+def bridge_out(tmp_path_factory):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert os.path.exists(BIN), "bridge_test not built (raytracing_test_amd/build.py build_bridge_test)"
+    out = str(tmp_path_factory.mktemp("bridge") / "out.json")
+    p = subprocess.run([BIN, out], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-2000:])
+    return json.load(open(out))
+
+
+def _ray(r):
+    return (tuple(r.pos), tuple(r.last), r.steps)
+
+
+def _got(v):
+    return (tuple(v[:3]), tuple(v[3:6]), v[6])
+
+
+def test_bridge_sequence_vs_oracle(rt, oracle_mod, bridge_out):
+    T = oracle_mod.Tree.reference_world()
+    n = oracle_mod.normalize
+    assert _got(bridge_out["pick_default"]) == _ray(T.cast_ray((35, 50, 35), n((1, 0, 1)), 30))
+    assert _got(bridge_out["pick_c1"]) == _ray(T.cast_ray((4.0, 90.0, 4.0), n((1, -0.45, 1)), 300))  # a miss
+    c1, d1 = (35.0, 60.0, 35.0), n((1, -0.6, 1))
+    a = T.cast_ray(c1, d1, 300)
+    assert a.hit and _got(bridge_out["pick_edit"]) == _ray(a)
+    assert tuple(bridge_out["block_c1"]) == T.get_block(*a.pos)[:2]
+    # input.cpp:146 deleteBlock(pos, 6), then :157 putBlock(lastPos, block, 6)
+    assert T.delete_block(*a.pos, level=6)[0] == 0
+    b = T.cast_ray(c1, d1, 300)
+    assert _got(bridge_out["after_delete"]) == _ray(b)
+    assert T.put_block(*b.last, 0x2, 123456789, 0.0, 6) == 0
+    c = T.cast_ray(c1, d1, 300)
+    assert _got(bridge_out["after_put"]) == _ray(c)
+    assert tuple(c.pos) == tuple(b.last)  # the new block is what the pick ray hits now
+    # a 4^3 block (putBlock level 5), then the reference's deleteBlock level 5: one voxel of it
+    assert T.put_block(20, 80, 20, 0, 777, 0.0, 5) == 0
+    assert T.delete_block(20, 80, 20, level=5)[0] == 0
+    assert bridge_out["level_edits"] == [T.get_block(20, 80, 20)[1], T.get_block(21, 80, 20)[1]] == [0xFFFFFFFFFFFFFFFF, 777]
+    # the primary-ray frame of the edited world (64 x 48, S = 300)
+    ref = T.cast_frame(c1, d1, 64, 48, 300)
+    fr = np.array(bridge_out["frame"], np.int64).reshape(-1, 4)
+    assert np.array_equal(fr[:, :3], ref["pos"]) and np.array_equal(fr[:, 3], ref["steps"])
+    assert bridge_out["shade_finite"] == 1
+
+
+def test_bridge_single_rank_exchange(bridge_out):
+    """svo_exchange_frames over a one-rank RCCL communicator: the unpacked frames equal the cast
+    records bit for bit (hit records and AO counts)"""
+    assert bridge_out["exchange_equal"] == 1
+    assert bridge_out["exchange_hits"] > 0

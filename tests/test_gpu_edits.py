@@ -66,3 +66,44 @@ def test_sync_after_rebuild_and_growth(rt, torch_cuda):
     cam = rt.normalize((1.0, -0.3, 0.7))
     _frames_equal(rt, tree.cast_frame((-20.5, 180.0, -10.0), cam, 256, 144, 600), fresh.cast_frame((-20.5, 180.0, -10.0), cam, 256, 144, 600),
                   "growth")
+
+
+def test_patched_tree_casts_match_oracle(rt, oracle_mod, torch_cuda):
+    """svo_tree_update + svo_tree_sync after a putBlock / deleteBlock sequence (levels 6 / 5 / 4) on the
+    GPU vs the oracle's reference-layout tree after the same edits (tests/test_edits.py
+    _oracle_edit_replay: putBlock tetrahexa_tree.cpp:176-291, deleteBlock :293-359): every cast field
+    bit-exact, frames at two poses and budgets; the shading pass over the patched tree equals the
+    one over a fresh upload."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_edits import _oracle_edit_replay
+
+    w = rt.World.reference()
+    tree = w.build().upload(0)
+
+    def on_edit(pts, lv):
+        tree.update(w, pts, level=lv)
+        tree.sync()
+
+    _, T, edits = _oracle_edit_replay(oracle_mod, np.random.default_rng(17), w=w, on_edit=on_edit)
+    pal = tree.palette()
+    pf = np.array([p[0] for p in pal], np.uint32)
+    pc = np.array([p[1] for p in pal], np.uint64)
+    for org, cd in (((35.0, 50.0, 35.0), (1.0, 0.0, 1.0)), ((4.0, 90.0, 4.0), (1.0, -0.45, 1.0)),
+                    ((60.5, 75.25, 20.75), (0.4, -0.5, 1.0))):
+        cam = rt.normalize(cd)
+        for S in (30, 300):
+            g = rt.decode_hits(tree.cast_frame(org, cam, 256, 192, S))
+            ref = T.cast_frame(org, cam, 256, 192, S)
+            assert ref["rc"] == 0
+            assert np.array_equal(g["pos"], ref["pos"]) and np.array_equal(g["steps"], ref["steps"]), (org, S)
+            assert np.array_equal(g["hit"], ref["hit"] != 0) and np.array_equal(g["last_pos"], ref["last"]), (org, S)
+            mid = np.where(g["hit"], g["material"], 0)
+            assert np.array_equal(pf[mid], ref["flags"]) and np.array_equal(pc[mid], ref["color"]), (org, S)
+            assert np.array_equal(g["t"], ref["t"].astype(np.float32)), (org, S)
+    fresh = w.build().upload(0)
+    a = tree.shade_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 240, 136, 300, sun=rt.sun_dir())
+    b = fresh.shade_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 240, 136, 300, sun=rt.sun_dir())
+    assert torch_cuda.equal(a, b)

@@ -307,9 +307,9 @@ def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):
 
 @pytest.fixture(scope="module")
 def depth12(rt, torch_cuda):
-    t = rt.Tree.terrain(6, 4096, 4096)
-    t.upload(0)
-    return t
+    # the tree bench.py times: noise + build on the GPU (svo_build_terrain_gpu), so the
+    # C3 / C4 parity below pins the on-device builder to the oracle as well
+    return rt.Tree.terrain_gpu(6, 4096, 4096, 0)
 
 
 def test_depth12_sampled_parity(rt, oracle_mod, depth12):
@@ -424,7 +424,7 @@ def test_depth14_4k_sampled_parity(rt, oracle_mod, torch_cuda):
     """C5: depth-14 (16384^2 columns, 7 levels), 3840x2160 from the C1 pose; sampled pixels against the
     oracle's 7-level reference-format tree over the first 4096^2 columns (every ray of this pose lands
     within ~2,600 voxels; the full reference-format tree would exceed its 2^32-byte pools)."""
-    t = rt.Tree.terrain(7, 16384, 16384, nthreads=16).upload(0)
+    t = rt.Tree.terrain_gpu(7, 16384, 16384, 0)  # the tree bench.py --config c5 times
     T = oracle_mod.Tree.terrain(7, 4096, 4096, nthreads=16)
     dn = rt.normalize([1, -0.45, 1])
     W, H = 3840, 2160
