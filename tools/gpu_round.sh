@@ -12,7 +12,7 @@ export TMPDIR=/tmp
 fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -gt 128 ]; }
 
 echo "[gpu_round] $(date) pytest" | tee -a "$OUT/steps.log"
-timeout -k 10 1200 python -m pytest tests -m gpu -q -x "$@" > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > "$OUT/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/steps.log"; tail -5 "$OUT/pytest_gpu.log"
 if fatal $rc; then exit $rc; fi
 
