@@ -1,24 +1,35 @@
 #!/usr/bin/env python3
 """bench.py — primary rays/s of the gfx950 SVO raycaster on BASELINE.json's metric config.
 
-Workload: genWorld's terrain on 4096 x 4096 columns as a depth-12
-(4096^3, 6-level) tree, one 1920x1080 frame of primary rays from (4,90,4) towards
+Workload (the default): genWorld's terrain on 4096 x 4096 columns as a
+depth-12 (4096^3, 6-level) tree, one 1920x1080 frame of primary rays from (4,90,4) towards
 normalize(1,-0.45,1), step budget 16384, castRayFromCam semantics (every ray ends on terrain).
-A "step" = one frame per GPU: with N ranks, N frames (camera poses shifted along the diagonal)
-are each sharded over all ranks by interleaved 8-pixel tile rows (row r -> rank r mod N), every
-rank casts its rows of every frame, and the hit records are gathered to rank 0 over RCCL.
-Per-GPU work is fixed as N grows ("weak").  Inputs (tree, camera) are resident in HBM before
-the timed region; the timed region is K steps between barrier + synchronize on both sides; the
-reported time is the max over ranks.
+Other configs: --config c1 (dense 256^3 grid, 256^2 rays), c2 / c2cam0 (the reference world),
+c5 (depth-14, 4K); --ao N (C4: + N hemisphere AO rays per hit); --shade (the shading pass).
+
+A "step" = one pass of the cast kernel over the step's frames.  Multi-GPU (one process per GPU,
+torch.distributed.run): frames are sharded by interleaved 8-pixel tile rows (row r -> rank r mod N)
+and every frame's shards are gathered over RCCL to the rank that displays it, by the C ABI's
+svo_exchange_frames (include/svo_rt.h), overlapped with the next step's cast on a second stream.
+  * default ("weak"): a step renders N frames (camera poses shifted along the diagonal), so per-GPU
+    work is fixed as N grows; frame f is displayed by rank f (the gathers form one all-to-all);
+  * --frames F ("strong"): a step renders F frames whatever N is (C5 as BASELINE.json words it:
+    --config c5 --frames 1 = one 4K frame split over N GPUs, gathered to rank 0).
+Inputs (tree, camera) are resident in HBM before the timed region; the timed region is K steps
+between barrier + synchronize on both sides; the reported time is the max over ranks.
 
 Extra objects on the JSON line:
   roofline     — the cast kernel's algorithmic bytes (B_ray = 16*E_node +
-                 4*E_child + B_out per ray, E from profiles/bray.json) / its average launch time,
-                 measured with HIP events on the launch stream (N=1: one pair around the timed
-                 region, gaps between launches included), against the 8 TB/s HBM peak;
-                 traffic = HBM bytes per launch from the committed rocprofv3 PMC pass (or null).
-  cpu_baseline — the oracle's C restatement of castRayFromCam + getBlock (reference layout, full
-                 descent per step) timed on this host's cores on the same frame (rank 0, N=1).
+                 4*E_child + B_out per ray (+ the AO rays' entries for C4), E from profiles/bray.json)
+                 / its average launch time, measured with HIP events on the launch stream, against
+                 the 8 TB/s HBM peak (`frac`); next to it what the committed rocprofv3 PMC passes of
+                 the same config (profiles/pmc_<config>.json) measured: HBM bytes per launch
+                 (`traffic`), measured HBM GB/s, L2 hit rate, VALU / SALU instructions per wave and
+                 the VALU issue fraction; `bound` names the larger of the measured HBM and VALU-issue
+                 fractions.
+  cpu_baseline — the oracle's C restatement of castRayFromCam + getBlock (reference node/array
+                 layout, full descent per step) timed on this host's cores on the same workload
+                 (rank 0, N=1), plus config C1 (dense grid) every time.
 """
 import argparse
 import json
@@ -32,98 +43,244 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-LEVELS, COLS = 6, 4096
-W, H = 1920, 1080
-ORIGIN = (4.0, 90.0, 4.0)
-CAM = (1.0, -0.45, 1.0)
-STEPS = 16384
+N_SIMD = 1024  # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4  # peak engine clock (the VALU issue fraction is priced at it: a lower bound on busy)
+VALU_CYCLES = 2  # a wave64 VALU instruction occupies a SIMD for 2 cycles (f64 ops: more)
 B_OUT = 24  # hit record bytes per ray (int4 pos+steps, f32 t, u32 info)
 
-
-FRAME_SHIFT = 64.0  # camera shift along the diagonal between the frames of one step (N > 1)
-BRAY_KEY = {"c2": "C2_cam1_S300", "c2cam0": "C2_cam0_S300", "c3": "C3", "c5": "C5"}
-
-
-def frame_origin(f):
-    return (ORIGIN[0] + FRAME_SHIFT * f, ORIGIN[1], ORIGIN[2] + FRAME_SHIFT * f)
-
-
-def load_bray(config="c3"):
-    p = os.path.join(ROOT, "profiles", "bray.json")
-    if os.path.exists(p):
-        d = json.load(open(p))
-        c = d.get(BRAY_KEY[config])
-        if c:
-            return c["e_child_per_ray"], d
-    return None, None
-
-
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(p):
-        d = json.load(open(p))
-        return d.get("hbm_bytes_per_launch"), d
-    return None, None
+# config -> scene / camera / budget
+CONFIGS = {
+    "c1": dict(levels=4, cols=256, W=256, H=256, origin=(35.0, 50.0, 35.0), cam=(1.0, 0.0, 1.0), steps=300, shift=4.0,
+               label="C1: the reference world's [0,256)^3 as a 256^3 grid (4 levels), 256x256", bray="C1",
+               metric="primary rays/sec at 256x256, dense 256^3 grid (config 1)"),
+    "c2": dict(levels=5, cols=200, W=1920, H=1080, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=300, shift=8.0,
+               label="C2: the reference world (5 levels, 1024^3), 1920x1080", bray="C2_cam1_S300",
+               metric="primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline"),
+    "c2cam0": dict(levels=5, cols=200, W=1920, H=1080, origin=(35.0, 50.0, 35.0), cam=(1.0, 0.0, 1.0), steps=300, shift=8.0,
+                   label="C2: the reference world (5 levels, 1024^3), 1920x1080, the reference's default camera (globals.cpp:20-21)",
+                   bray="C2_cam0_S300",
+                   metric="primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline"),
+    "c3": dict(levels=6, cols=4096, W=1920, H=1080, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
+               label="C3: depth-12 SVO (4096^2 terrain columns, 6 levels, 4096^3), 1920x1080", bray="C3",
+               metric="primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
+    "c5": dict(levels=7, cols=16384, W=3840, H=2160, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
+               label="C5: depth-14 SVO (16384^2 terrain columns, 7 levels, 16384^3), 3840x2160", bray="C5",
+               metric="primary rays/sec at 4K, depth-14 SVO; achieved HBM GB/s vs roofline"),
+}
 
 
-def cpu_baseline(ppx, ppy, gpu_hits=None, config="c3"):
-    """Oracle (test infrastructure) timed on the host: the reference algorithm and layout."""
+def frame_origin(cfg, f):
+    o, s = cfg["origin"], cfg["shift"]
+    return (o[0] + s * f, o[1], o[2] + s * f)
+
+
+def run_key(args):
+    """the profiles/pmc_<key>.json a config's counters live in"""
+    return args.config + ("_ao%d" % args.ao if args.ao else "") + ("_shade" if args.shade else "")
+
+
+def load_json(name):
+    p = os.path.join(ROOT, "profiles", name)
+    return json.load(open(p)) if os.path.exists(p) else None
+
+
+# ------------------------------------------------------------------------------- CPU baseline --
+def cpu_info():
+    """The host's CPUs and the threads the baseline may use: the job's CPU allotment (OMP_NUM_THREADS,
+    which the GPU pool sets to the job's share of a shared host; else the affinity mask, capped by
+    a cgroup CPU quota)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(aff, quota) if quota else aff
+    rule = "affinity mask" + (" capped by the cgroup CPU quota" if quota else "")
+    if omp and omp.isdigit() and int(omp) > 0:
+        threads, rule = min(int(omp), aff), "OMP_NUM_THREADS (the job's CPU share on this host)"
+    return {"nproc": nproc, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "cpu_model": model, "threads": threads,
+            "threads_rule": rule}
+
+
+def _timed(fn):
+    t0 = time.perf_counter()
+    r = fn()
+    return r, time.perf_counter() - t0
+
+
+def cpu_baseline(args, cfg, ppx, ppy, gpu):
+    """The oracle (test infrastructure: the reference algorithm + layout, oracle/oracle.c) timed on
+    this host's cores: all allotted threads on the workload (or a stated sample of it), one thread
+    on a fixed strided sample; parity of the GPU frame on the same rays."""
     from oracle import oracle as O
 
     O.build(native=True)
-    cores = min(16, os.cpu_count() or 1)
-    t0 = time.time()
-    T = O.Tree.reference_world() if config.startswith("c2") else O.Tree.terrain(LEVELS, COLS, COLS, native=True, nthreads=cores)
-    build_s = time.time() - t0
-    dn = O.normalize(CAM)
-    rng = np.random.default_rng(1)
-    pix = np.sort(rng.choice(W * H, W * H // 4, replace=False))
-    t0 = time.time()
-    ref = T.cast_frame(ORIGIN, dn, W, H, STEPS, ppx=ppx, ppy=ppy, pixels=pix, nthreads=cores)
-    dt = time.time() - t0
-    one = pix[:: 64]
-    t1 = time.time()
-    T.cast_frame(ORIGIN, dn, W, H, STEPS, ppx=ppx, ppy=ppy, pixels=one, nthreads=1)
-    dt1 = time.time() - t1
+    ci = cpu_info()
+    nt = ci["threads"]
+    W, H, S = cfg["W"], cfg["H"], cfg["steps"]
+    dn = O.normalize(cfg["cam"])
+    org = cfg["origin"]
+    t0 = time.perf_counter()
+    if args.config.startswith("c2") or args.config == "c1":
+        T = O.Tree.reference_world(native=True)
+    elif args.config == "c5":
+        # every C5 ray lands within ~2,600 voxels of the camera: the oracle's tree over the first 4096^2
+        # columns holds the same voxels (its pools cannot hold 16384^2; tests/test_gpu_parity.py)
+        T = O.Tree.terrain(7, 4096, 4096, native=True, nthreads=nt)
+    else:
+        T = O.Tree.terrain(cfg["levels"], cfg["cols"], cfg["cols"], native=True, nthreads=nt)
+    build_s = time.perf_counter() - t0
+    n = W * H
+    # the multi-thread leg: the whole frame unless that is far beyond ~10-30 s of CPU work
+    stride = {"c5": 8}.get(args.config, 1) * (4 if args.ao else 1) * (4 if args.shade else 1)
+    stride1 = 16 * stride  # the single-thread leg: every 16th of those rays
+    pix = np.arange(0, n, stride, dtype=np.int64)
+    pix1 = np.arange(0, n, stride1, dtype=np.int64)
+    parity = None
+    if args.config == "c1":
+        D = O.Dense(T, 256)
+        ref, dt = _timed(lambda: D.cast_frame(org, dn, W, H, S, nthreads=nt))
+        _, dt1 = _timed(lambda: D.cast_frame(org, dn, W, H, S, nthreads=1))
+        pix1 = pix
+        if gpu is not None:
+            parity = bool(np.array_equal(gpu["pos"], ref["pos"]) and np.array_equal(gpu["steps"], ref["steps"]))
+        what = "castRayFromCam over a dense u8 grid (getBlock seam ray_caster.cpp:81, coordinates & 255)"
+    elif args.shade:
+        sun = np.asarray(O.normalize((2.0, 1.0, 4.0)))
+        ref, dt = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt))
+        _, dt1 = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1))
+        if gpu is not None:
+            parity = bool(np.abs(gpu["rgba"][pix] - ref).max() <= 2e-6)
+        what = "the shading pass (oracle orc_shade_frame: castRayFromCam + reflections + 75-step shadow ray)"
+    elif args.ao:
+        (ao, hit), dt = _timed(lambda: T.cast_frame_ao(org, dn, W, H, S, args.ao, 5, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt))
+        _, dt1 = _timed(lambda: T.cast_frame_ao(org, dn, W, H, S, args.ao, 5, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1))
+        if gpu is not None:
+            parity = bool(np.array_equal(gpu["ao"][pix], ao) and np.array_equal(gpu["hit"][pix], hit != 0))
+        what = "castRayFromCam + %d hemisphere AO rays of 5 steps per hit (oracle orc_cast_frame_ao)" % args.ao
+    else:
+        ref, dt = _timed(lambda: T.cast_frame(org, dn, W, H, S, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt))
+        _, dt1 = _timed(lambda: T.cast_frame(org, dn, W, H, S, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1))
+        if gpu is not None:
+            parity = bool(np.array_equal(gpu["pos"][pix], ref["pos"]) and np.array_equal(gpu["steps"][pix], ref["steps"]))
+        what = "castRayFromCam + getBlock on the reference node/array layout"
     res = {
         "value": len(pix) / dt,
         "unit": "rays/s",
-        "cores": cores,
+        "cores": nt,
         "kind": "port",
-        "sample": "%d random pixels (1/4) of the same 1080p %s frame, %d threads; oracle/oracle.c (-O3 -march=native "
-                  "-ffp-contract=off) restating castRayFromCam + getBlock on the reference node/array layout" % (len(pix), config.upper(), cores),
-        "single_thread_rays_per_s": len(one) / dt1,
+        "sample": "%s of the %dx%d %s frame (every %d-th pixel), %d threads; single thread: every %d-th pixel (%d rays); "
+                  "oracle/oracle.c (-O3 -march=native -ffp-contract=off): %s"
+                  % ("all %d rays" % n if stride == 1 else "%d rays" % len(pix), W, H, args.config.upper(), stride, nt, stride1 if
+                     args.config != "c1" else stride, len(pix1), what),
+        "single_thread_rays_per_s": len(pix1) / dt1,
+        "cpu_s": round(dt + dt1, 2),
         "tree_build_s": round(build_s, 2),
+        **{k: ci[k] for k in ("nproc", "affinity_cpus", "cgroup_quota_cpus", "cpu_model", "threads_rule")},
     }
-    if gpu_hits is not None:
-        g = gpu_hits
-        res["parity_vs_gpu"] = bool(np.array_equal(g["pos"][pix], ref["pos"]) and np.array_equal(g["steps"][pix], ref["steps"]))
+    if parity is not None:
+        res["parity_vs_gpu"] = parity
+    if args.config != "c1" and not args.no_c1:
+        res["c1"] = cpu_c1(O, nt)
     return res
 
 
+def cpu_c1(O, nt):
+    """Config C1 (BASELINE.json configs[0]: the CPU reference path only): the reference world's
+    [0,256)^3 materialised as a dense grid, castRayFromCam over it (getBlock seam ray_caster.cpp:81),
+    256^2 rays from the reference camera (35,50,35)->(1,0,1), S = 300."""
+    T = O.Tree.reference_world(native=True)
+    D = O.Dense(T, 256)
+    dn = O.normalize((1.0, 0.0, 1.0))
+    r, dt = _timed(lambda: D.cast_frame((35.0, 50.0, 35.0), dn, 256, 256, 300, nthreads=nt))
+    _, dt1 = _timed(lambda: D.cast_frame((35.0, 50.0, 35.0), dn, 256, 256, 300, nthreads=1))
+    return {"rays_per_s": 65536 / dt, "single_thread_rays_per_s": 65536 / dt1, "threads": nt,
+            "dda_steps_per_ray": r["dda_steps"] / 65536.0,
+            "workload": "C1: dense 256^3 grid of the reference world, 256x256 rays, (35,50,35)->normalize(1,0,1), S=300"}
+
+
+# ---------------------------------------------------------------------------------- roofline --
+def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
+    bray = load_json("bray.json") or {}
+    key = cfg["bray"] if not args.ao else "C4_ao%d" % args.ao
+    b = bray.get(key)
+    if args.shade or b is None:
+        model = None  # §8(d) prices primary traversal (+ AO); the shading pass has no such model
+    else:
+        model = b["bytes_per_ray"]
+    achieved = model * rays_per_launch / avg_kernel_s / 1e9 if model else None
+    roof = {"bound": None, "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": None,
+            "bytes_per_ray": round(model, 2) if model else None, "bytes_model": "SURVEY.md §8d (%s, profiles/bray.json)" % key if model else None,
+            "avg_launch_ms": round(avg_kernel_s * 1e3, 4), "rays_per_launch": rays_per_launch}
+    pmc = load_json("pmc_%s.json" % run_key(args))
+    if pmc and pmc.get("rays_per_launch"):
+        c = pmc["counters_per_dispatch"]
+        scale = rays_per_launch / pmc["rays_per_launch"]  # per-ray figures of the N=1 pass, this launch's rays
+        traffic = pmc["hbm_bytes_per_launch"] * scale
+        hbm = traffic / avg_kernel_s / 1e9
+        valu = c["SQ_INSTS_VALU"] * scale
+        valu_frac = valu * VALU_CYCLES / (N_SIMD * CLOCK_GHZ * 1e9 * avg_kernel_s)
+        roof.update({
+            "traffic": round(traffic), "hbm_gbs_measured": round(hbm, 1), "hbm_frac_measured": round(hbm / HBM_PEAK_GBS, 4),
+            "l2_hit_rate": round(pmc["l2_hit_rate"], 4) if pmc.get("l2_hit_rate") is not None else None,
+            "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1),
+            "salu_insts_per_wave": round(c["SQ_INSTS_SALU"] / c["SQ_WAVES"], 1) if "SQ_INSTS_SALU" in c else None,
+            "valu_issue_frac": round(valu_frac, 4),
+            "bound": "valu-issue" if valu_frac > hbm / HBM_PEAK_GBS else "hbm",
+            "counters": "profiles/pmc_%s.json (rocprofv3 --pmc passes, tools/pmc.sh%s)" % (run_key(args), "; scaled per ray to this launch"
+                                                                                          if world > 1 or scale != 1 else ""),
+            "valu_issue_rule": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz x launch time)" % (VALU_CYCLES, N_SIMD, CLOCK_GHZ),
+        })
+    elif model:
+        roof["bound"] = "hbm"  # the §8(d) model's bound; no counters committed for this config
+    return roof
+
+
+# ------------------------------------------------------------------------------------- main --
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
+                    help="c3: depth-12 / 1080p (the metric); c5: depth-14 / 4K; c2: the reference world / 1080p / S=300 from the "
+                         "C3 pose, c2cam0 from the reference's default camera; c1: the dense 256^3 grid, 256^2 rays")
+    ap.add_argument("--frames", type=int, default=None,
+                    help="frames per step over all GPUs (strong scaling; default: one per GPU, weak scaling)")
+    ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
+    ap.add_argument("--shade", action="store_true",
+                    help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 CPU timing inside cpu_baseline")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: cast only, no exchange")
+    ap.add_argument("--exchange", default="capi", choices=["capi", "torch"],
+                    help="capi: svo_exchange_frames (RCCL inside libsvo_rt); torch: all_to_all_single of wire records")
+    ap.add_argument("--force-exchange", action="store_true", help="run the exchange at N=1 too (a one-rank RCCL communicator)")
     ap.add_argument("--cols", type=int, default=None)
-    ap.add_argument("--config", default="c3", choices=["c2", "c2cam0", "c3", "c5"],
-                    help="c3: depth-12 / 1080p (the metric); c5: depth-14 (16384^2 columns, 7 levels) / 3840x2160; c2: the "
-                         "reference world (initTetraHexaTree + genWorld, 5 levels) / 1080p / S=300 from the C3 pose, c2cam0 "
-                         "from the reference's default camera")
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
-    ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
     ap.add_argument("--host-build", action="store_true", help="build the tree on the host (default: svo_build_terrain_gpu)")
-    ap.add_argument("--shade", action="store_true",
-                    help="SURVEY §8f.1: shaded frames (svo_shade_rays: primary + reflections + 75-step sun shadow ray), "
-                         "rgba gathered instead of hit records")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU; torch exchange)")
     ap.add_argument("--verify", action="store_true",
-                    help="N>1: rank 0 checks the gathered, unpacked records of every frame against a one-GPU cast of it")
+                    help="with an exchange: every rank checks the frames it displays against a one-GPU cast of them")
     ap.add_argument("--launch-events", action="store_true",
                     help="an event pair around every cast launch (default at N=1: one pair around the timed region, whose "
                          "average per launch includes the gaps between launches; per-launch pairs cost ~7 us per step)")
@@ -133,6 +290,7 @@ def main():
     import torch.distributed as dist
 
     import raytracing_test_amd as rt
+    from raytracing_test_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -144,132 +302,128 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(args.dist_backend)
+    cfg = dict(CONFIGS[args.config])
+    if args.cols is not None:
+        cfg["cols"] = args.cols
+    W, H, STEPS = cfg["W"], cfg["H"], cfg["steps"]
+    if args.shade and args.ao:
+        ap.error("--shade and --ao are separate workloads")
 
-    global LEVELS, W, H, ORIGIN, CAM, STEPS, FRAME_SHIFT
-    if args.config.startswith("c2"):
-        LEVELS, STEPS, FRAME_SHIFT = 5, 300, 8.0
-        if args.config == "c2cam0":  # globals.cpp:20-21
-            ORIGIN, CAM = (35.0, 50.0, 35.0), (1.0, 0.0, 1.0)
-    if args.config == "c5":
-        LEVELS, W, H = 7, 3840, 2160
-        args.no_cpu_baseline = True  # the reference-format CPU tree of 16384^2 terrain exceeds its 2^32-byte pools
-    if args.cols is None:
-        args.cols = 4096 if args.config == "c3" else 16384
+    # ---- the tree, resident in HBM before timing
     t0 = time.time()
-    if args.config.startswith("c2"):  # initTetraHexaTree + genWorld, putBlock by putBlock
+    builder = "gpu"
+    if args.config == "c1":  # the reference world's [0,256)^3, voxel by voxel (product getBlock / putBlock)
+        ref = rt.World.reference()
+        g = np.stack(np.meshgrid(np.arange(256), np.arange(256), np.arange(256), indexing="ij"), -1).reshape(-1, 3).astype(np.int32)
+        bf, bc, _ = ref.get_blocks(g)
+        stored = bc != np.uint64(0xFFFFFFFFFFFFFFFF)
+        w4 = rt.World(4)
+        w4.put_blocks(g[stored], bf[stored] & ~np.uint32(1), bc[stored])
+        tree = w4.build()
+        builder = "host (putBlock)"
+        build_s = time.time() - t0
+        tree.upload(dev)
+    elif args.config.startswith("c2"):  # initTetraHexaTree + genWorld, putBlock by putBlock
         tree = rt.World.reference().build()
+        builder = "host (putBlock)"
         build_s = time.time() - t0
         tree.upload(dev)
     elif args.host_build:
-        tree = rt.Tree.terrain(LEVELS, args.cols, args.cols, nthreads=16)
+        tree = rt.Tree.terrain(cfg["levels"], cfg["cols"], cfg["cols"], nthreads=16)
+        builder = "host"
         build_s = time.time() - t0
         tree.upload(dev)
     else:  # noise + build in HBM (identical arrays, tests/test_gpu_build.py); already uploaded
-        tree = rt.Tree.terrain_gpu(LEVELS, args.cols, args.cols, dev)
+        tree = rt.Tree.terrain_gpu(cfg["levels"], cfg["cols"], cfg["cols"], dev)
         build_s = time.time() - t0
     info = tree.info()
     ppx, ppy = rt.proj_plane(W, H)
-    cam = rt.normalize(CAM)
+    cam = rt.normalize(cfg["cam"])
 
-    from raytracing_test_amd import shard
-
-    nframes = world
-    # one launch per step covers this rank's tile rows of all N frames (each frame's shard alone
-    # would fill 1/N of the GPU); records of frame f follow those of frame f-1
-    origins = [frame_origin(f) for f in range(nframes)]
-    desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
-                              flags=(rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags, ao_samples=args.ao,
-                              frame_origins=origins if nframes > 1 else None)
-    descs = [desc]
-    gather = world > 1 and not args.no_gather
-    # The exchange: frame f is displayed by rank f, so every frame's tile-row shards are gathered to
-    # its own rank — one all-to-all per step (rank r sends its rows of frame f to rank f), which
-    # spreads the traffic over every rank's xGMI links instead of funnelling N frames into rank 0.
-    # Hit records travel as 12-B wire records (svo_hits_pack); the image (--shade) and AO counts as
-    # they are.
-    wire_fmt = gather and not args.shade
-    n_mine = rt.Tree.count(desc) // nframes  # my records of one frame
-    counts = [shard.shard_count(W, H, r, world) for r in range(world)]  # rank r's records of one frame
-    nbuf = 2 if gather else 1  # the exchange of step k overlaps the cast of step k+1
+    # ---- frames of a step and this rank's shard of them (one launch covers the shard of every frame)
+    strong = args.frames is not None
+    nframes = args.frames if strong else world
+    if not 1 <= nframes <= 16:
+        ap.error("1 <= frames per step <= 16 (SVO_MAX_FRAMES)")
+    origins = [frame_origin(cfg, f) for f in range(nframes)]
+    flags = (rt.CAST_ITERATIVE if args.iterative else 0) | args.cast_flags
+    desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world, flags=flags,
+                              ao_samples=args.ao, frame_origins=origins if nframes > 1 else None)
+    rays_per_launch = rt.Tree.count(desc)
+    gather = (world > 1 or args.force_exchange) and not args.no_gather
+    xmode = None
+    if gather:
+        xmode = "torch" if (args.shade or args.exchange == "torch" or args.dist_backend != "nccl") else "capi"
     gdev = torch.device("cuda", dev)
-    outs, sends, recvs = [], [], []
+    nbuf = 2 if gather else 1  # the exchange of step k overlaps the cast of step k+1
+    outs = []
     for _ in range(nbuf):
-        views = rt.Tree.alloc_hits(n_mine * nframes, dev, ao=args.ao > 0)
-        if args.shade:  # the image is the product: exchange it instead of the hit records
-            views["rgba"] = torch.zeros((n_mine * nframes, 4), dtype=torch.float32, device=gdev)
+        views = rt.Tree.alloc_hits(rays_per_launch, dev, ao=args.ao > 0)
+        if args.shade:
+            views["rgba"] = torch.zeros((rays_per_launch, 4), dtype=torch.float32, device=gdev)
         outs.append(views)
-        if gather:
-            snd, rcv = [], []
-            if wire_fmt:
-                snd.append(torch.zeros((n_mine * nframes, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
-                rcv.append(torch.zeros((W * H, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
-            if args.ao:
-                snd.append(views["ao"])
-                rcv.append(torch.zeros(W * H, dtype=torch.uint8, device=gdev))
-            if args.shade:
-                snd.append(views["rgba"])
-                rcv.append(torch.zeros((W * H, 4), dtype=torch.float32, device=gdev))
-            sends.append(snd)
-            recvs.append(rcv)
     stream = torch.cuda.Stream(device=dev)
-    src_descs, frame_hits = None, None
-    if wire_fmt:  # my frame (rank) from every rank's rows, unpacked into one record buffer
-        src_descs = [rt.Tree.frame_desc(origins[rank], cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world)
-                     for r in range(world)]
-        frame_hits = rt.Tree.alloc_hits(W * H, dev)
+    xstream = torch.cuda.Stream(device=dev) if gather else None
+    exch = None
+    xnote = None
+    n_own = len(range(rank, nframes, world))  # frames this rank displays
+    frames_out = None
+    if xmode == "capi":
+        try:
+            if world > 1:
+                uid = torch.zeros(rt.NCCL_UNIQUE_ID_BYTES, dtype=torch.uint8, device=gdev)
+                if rank == 0:
+                    uid.copy_(torch.frombuffer(bytearray(rt.Exchange.unique_id()), dtype=torch.uint8))
+                dist.broadcast(uid, 0)
+                uid = bytes(uid.cpu().numpy().tobytes())
+            else:
+                uid = rt.Exchange.unique_id()
+            exch = rt.Exchange(world, rank, uid, dev)
+        except rt.SvoError as e:  # keep the scaling run alive; say so on the line
+            xmode, xnote = "torch", "svo_exchange_create failed (%s); torch.distributed all_to_all used" % e
+        if exch is not None and n_own:
+            frames_out = rt.Tree.alloc_hits(n_own * W * H, dev, ao=args.ao > 0)
+
+    # torch exchange (shading image, gloo rehearsal, or --exchange torch): frame f -> rank f % world
+    counts = [shard.shard_count(W, H, r, world) for r in range(world)]
+    n_mine = counts[rank]
     offs = np.concatenate([[0], np.cumsum(counts)]).tolist()
-    pending = {}  # step -> (async all-to-all works, send buffers kept alive)
+    tx = None
+    if xmode == "torch":
+        tx = TorchExchange(args, rt, tree, dist, torch, gdev, W, H, STEPS, ppx, ppy, cam, origins, rank, world, counts, offs, n_mine,
+                           outs, nbuf)
 
-    def unpack_step(k):
-        """wait (nccl: on the stream) for the exchange of step k, then unpack my frame's records"""
-        works, _ = pending.pop(k)
-        for w in works:
-            w.wait()
-        b = k % nbuf
-        if args.dist_backend != "nccl":  # gloo rehearsal: received on the host
-            for i, h in enumerate(recv_host[b]):
-                recvs[b][i].copy_(h)
-        if wire_fmt:
-            for r in range(world):
-                part = {key: v[offs[r]:offs[r + 1]] for key, v in frame_hits.items()}
-                tree.unpack_hits(src_descs[r], recvs[b][0][offs[r]:offs[r + 1]], part, stream)
+    xdone = [None] * nbuf
+    cast_done = [torch.cuda.Event() for _ in range(nbuf)]
 
-    recv_host = None
-    if gather and args.dist_backend != "nccl":
-        recv_host = [[torch.empty_like(x, device="cpu") for x in rcv] for rcv in recvs]
-
-    def one_step(k, events=None):
+    def one_step(k, ev=None):
         b = k % nbuf
         with torch.cuda.stream(stream):
-            if events is not None:
-                events[0][0].record(stream)
+            if xdone[b] is not None:
+                stream.wait_event(xdone[b])  # the exchange that read this buffer set has passed
+            if ev is not None:
+                ev[0].record(stream)
             if args.shade:
                 tree.shade(desc, outs[b]["rgba"], out=outs[b], stream=stream)
             else:
                 tree.cast(desc, outs[b], stream)
-            if events is not None:
-                events[0][1].record(stream)
-            if not gather:
-                return
-            if wire_fmt:
-                tree.pack_hits(desc, outs[b], sends[b][0], stream)
-            # asynchronous: the next step's cast runs while RCCL moves this one over xGMI (gloo
-            # rehearsal: the same pipeline through host copies); the unpack of step k-1 follows
-            works, keep = [], []
-            for i, (snd, rcv) in enumerate(zip(sends[b], recvs[b])):
-                src = snd if args.dist_backend == "nccl" else snd.cpu()
-                dst = rcv if args.dist_backend == "nccl" else recv_host[b][i]
-                works.append(dist.all_to_all_single(dst, src, output_split_sizes=counts, input_split_sizes=[n_mine] * world,
-                                                    async_op=True))
-                keep.append(src)
-            pending[k] = (works, keep)
-            if (k - 1) in pending:
-                unpack_step(k - 1)
+            if ev is not None:
+                ev[1].record(stream)
+        if not gather:
+            return
+        if xmode == "capi":
+            cast_done[b].record(stream)
+            xstream.wait_event(cast_done[b])
+            exch.frames(tree, desc, outs[b], frames_out, xstream)
+            e = torch.cuda.Event()
+            e.record(xstream)
+            xdone[b] = e
+        else:
+            xdone[b] = tx.step(k, b, stream)
 
     def drain():
-        with torch.cuda.stream(stream):
-            for k in sorted(pending):
-                unpack_step(k)
+        if tx is not None:
+            tx.drain(stream)
 
     step_no = 0
     for _ in range(args.warmup):
@@ -280,18 +434,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    evs = [[[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps)]
     reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-    # at N=1 the launches run back to back on one stream: one event pair around the timed region
-    # gives their average (gaps included); with a gather in between, pairs around each launch
-    args.region_events = world == 1 and not args.launch_events
+    # back-to-back launches on one stream: one event pair around the timed region gives their average
+    # (gaps included); with an exchange in between, pairs around each launch
+    region_events = not gather and not args.launch_events
     t0 = time.perf_counter()
-    if args.region_events:
+    if region_events:
         reg[0].record(stream)
     for k in range(args.steps):
-        one_step(step_no, None if args.region_events else evs[k])
+        one_step(step_no, None if region_events else evs[k])
         step_no += 1
-    if args.region_events:
+    if region_events:
         reg[1].record(stream)
     drain()
     torch.cuda.synchronize()
@@ -299,89 +453,56 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if args.region_events:  # launches back to back on one stream (no gather in between at N=1)
-        kern_ms = [reg[0].elapsed_time(reg[1]) / args.steps]
-    else:
-        kern_ms = [e[0].elapsed_time(e[1]) for step in evs for e in step]
+    kern_ms = [reg[0].elapsed_time(reg[1]) / args.steps] if region_events else [e[0].elapsed_time(e[1]) for e in evs]
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     total_rays = W * H * nframes * args.steps  # every rank's share of every frame, all steps
     value = total_rays / elapsed
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
-    rays_per_launch = rt.Tree.count(descs[0])
+
     verified = None
-    if args.verify and wire_fmt:
-        # my frame reassembled from every rank's unpacked records == a one-GPU cast of it
+    if args.verify and gather and not args.shade:
         torch.cuda.synchronize()
-        one = rt.decode_hits(tree.cast_frame(origins[rank], cam, W, H, STEPS, ppx, ppy, flags=args.cast_flags))
-        got = rt.decode_hits(frame_hits)
         ok = True
-        for r in range(world):
-            rows = shard.shard_pixel_rows(H, r, world)
-            idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
-            ok &= all(np.array_equal(got[key][offs[r]:offs[r + 1]], one[key][idx]) for key in ("pos", "steps", "hit", "axis", "material", "t"))
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        for k, f in enumerate(range(rank, nframes, world)):
+            one = rt.decode_hits(tree.cast_frame(origins[f], cam, W, H, STEPS, ppx, ppy, flags=flags, ao_samples=args.ao))
+            if xmode == "capi":
+                got = rt.decode_hits({key: v[k * W * H:(k + 1) * W * H] for key, v in frames_out.items()})
+                ok &= all(np.array_equal(got[key], one[key]) for key in got)
+            else:
+                ok &= tx.verify(f, one)
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=gdev)
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         verified = bool(flag.item())
 
     if args.stats and rank == 0:
-        d0 = descs[0]
-        nblk = rt.Tree.blocks(d0)
-        for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
-            st = torch.zeros(rt.STATS_HEADER + 2 * nblk + rt.Tree.count(d0), dtype=torch.int64, device=dev)
-            d0.flags |= mode
-            d0.stats = st.data_ptr()
-            tree.cast(d0, outs[0], stream)
-            torch.cuda.synchronize()
-            d0.flags &= ~mode
-            allv = st.cpu().numpy()
-            if mode == rt.CAST_STATS:
-                vals = allv[:rt.STATS_HEADER]
-                if os.environ.get("SVO_RAY_WORK"):  # per-pixel lookups / brick steps for offline analysis
-                    np.save(os.environ["SVO_RAY_WORK"], allv[rt.STATS_HEADER + 2 * nblk:])
-                per = [v / max(1, vals[0]) * (64 if k.startswith("wave_") and not k.endswith("_x64") else 1) for k, v in zip(rt.STAT_NAMES, vals)]
-                print("stats per ray (wave_* per wave): " + ", ".join("%s=%.3f" % (k, v) for k, v in zip(rt.STAT_NAMES, per)) +
-                      "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
-                continue
-            stamps = allv[rt.STATS_HEADER:rt.STATS_HEADER + 2 * nblk].reshape(-1, 2)
-            stamps = stamps[stamps[:, 1] > 0].astype(np.float64) / 100.0  # launched blocks; us (100 MHz)
-            t0s = stamps[:, 0].min()
-            dur = stamps[:, 1] - stamps[:, 0]
-            span = stamps[:, 1].max() - t0s
-            bins = np.linspace(0, span, 17)
-            res = [int(((stamps[:, 0] - t0s < b1) & (stamps[:, 1] - t0s > b0)).sum()) for b0, b1 in zip(bins[:-1], bins[1:])]
-            tenths = [float(np.mean(c)) for c in np.array_split(dur, 10)]
-            ends = np.sort(stamps[:, 1] - t0s)
-            print("timeline: span %.1f us, mean block %.1f us, max %.1f us, last 10%% of blocks end after %.1f us; blocks overlapping "
-                  "each 1/16 of the span %s; mean block us per tenth of the grid %s"
-                  % (span, dur.mean(), dur.max(), ends[int(len(ends) * 0.9)], res, ["%.0f" % x for x in tenths]), file=sys.stderr)
+        print_stats(rt, tree, desc, outs[0], stream, torch)
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
-    e_child, bray_meta = load_bray(args.config)
-    roof = None
-    if e_child is not None:
-        b_ray = 16.0 * (e_child + 1.0) + 4.0 * e_child + B_OUT
-        achieved = b_ray * rays_per_launch / avg_kernel_s / 1e9
-        traffic, _ = load_traffic() if args.config == "c3" else (None, None)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                "bytes_per_ray": round(b_ray, 2), "avg_launch_ms": round(avg_kernel_s * 1e3, 4)}
+    roof = roofline(args, cfg, rays_per_launch, avg_kernel_s, world)
     cpu = None
+    if world == 1 and nframes == 1 and not args.no_cpu_baseline:
+        gpu = None
+        if args.shade:
+            gpu = {"rgba": outs[0]["rgba"].cpu().numpy()}
+        else:
+            gpu = rt.decode_hits(outs[0])
+        cpu = cpu_baseline(args, cfg, ppx, ppy, gpu)
+    work = ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") + \
+           ("shaded (low_res.frag colour model, 75-step shadow rays): " if args.shade else "")
+    metric = cfg["metric"]
+    if args.ao:
+        metric = "primary rays/sec at 1080p with %d-sample hemisphere AO per hit, depth-12 SVO (config 4); achieved HBM GB/s vs roofline" % args.ao
     if args.shade:
-        roof = None  # the roofline model (§8d) prices primary traversal only
-    if world == 1 and not args.no_cpu_baseline and not args.ao and not args.shade:
-        hits = rt.decode_hits(outs[0])
-        cpu = cpu_baseline(ppx, ppy, hits, args.config)
+        metric = "shaded primary rays/sec (reflections + sun shadow ray)"
     line = {
-        "metric": ("shaded primary rays/sec (reflections + sun shadow ray)" if args.shade else
-                   {"c2": "primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline",
-                    "c2cam0": "primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline",
-                    "c3": "primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline",
-                    "c5": "primary rays/sec at 4K, depth-14 SVO; achieved HBM GB/s vs roofline"}[args.config]),
+        "metric": metric,
         "value": round(value, 1),
         "unit": "rays/s",
         "n_gpus": world,
@@ -389,37 +510,179 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": ("synthetic: the reference world (initTetraHexaTree + genWorld on 200x200 columns), built in-process"
-                 if args.config.startswith("c2") else
-                 "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (args.cols, args.cols)),
-        "config": {"ao_samples": args.ao, "shade": args.shade,
-                   "workload": ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") +
-                   ("shaded (low_res.frag colour model, 75-step shadow rays): " if args.shade else "") +
-                   {"c2": "C2: the reference world (5 levels, 1024^3), 1920x1080",
-                    "c2cam0": "C2: the reference world (5 levels, 1024^3), 1920x1080",
-                    "c3": "C3: depth-12 SVO (%d^2 terrain columns, 6 levels, 4096^3), 1920x1080" % args.cols,
-                    "c5": "C5: depth-14 SVO (%d^2 terrain columns, 7 levels, 16384^3), 3840x2160" % args.cols}[args.config] +
-                   " primary rays per GPU per step, camera (%g,%g,%g)->normalize(%g,%g,%g), S=%d, castRayFromCam semantics"
-                   % (ORIGIN + CAM + (STEPS,)),
-                   "frames_per_step": nframes, "rays_per_step": W * H * nframes, "parallelism": "tile-row shard x%d" % world,
-                   "launches_per_step": 1, "gather": gather,
-                   "exchange": ("frame f gathered to rank f (one all-to-all per step, overlapped with the next cast): " +
-                                ("rgba image" if args.shade else "12-B wire hit records (svo_hits_pack), unpacked on arrival" +
-                                 (" + AO counts" if args.ao else ""))) if gather else None, "tree_nodes": info.n_nodes,
-                   "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
-                   "tree_builder": "host" if args.host_build else "gpu"},
+                 if args.config in ("c1", "c2", "c2cam0") else
+                 "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (cfg["cols"], cfg["cols"])),
+        "config": {"workload": work + cfg["label"] + " primary rays per frame, camera (%g,%g,%g)->normalize(%g,%g,%g), S=%d, "
+                                                     "castRayFromCam semantics" % (cfg["origin"] + cfg["cam"] + (STEPS,)),
+                   "ao_samples": args.ao, "shade": args.shade, "frames_per_step": nframes, "rays_per_step": W * H * nframes,
+                   "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "gather": gather,
+                   "exchange": None if not gather else (
+                       ("svo_exchange_frames (C ABI, RCCL send/recv group): 12-B wire records" + (" + AO counts" if args.ao else "") +
+                        ", frame f to rank f %% N, unpacked on arrival, on a second stream overlapping the next cast")
+                       if xmode == "capi" else
+                       ("torch.distributed all_to_all_single: " + ("rgba image" if args.shade else "12-B wire hit records") +
+                        ", frame f to rank f %% N" + ("; " + xnote if xnote else ""))),
+                   "tree_nodes": info.n_nodes, "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
+                   "tree_builder": builder},
         "roofline": roof,
         "cpu_baseline": cpu,
         **({"gather_verified": verified} if verified is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
-                         "included)" if args.region_events else "a HIP event pair around every launch on its stream",
+                         "included)" if region_events else "a HIP event pair around every launch on its stream",
     }
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class TorchExchange:
+    """The exchange through torch.distributed (the shaded image, gloo rehearsals, --exchange torch):
+    frame f's tile-row shards to rank f % N by one all_to_all_single per buffer, wire records packed
+    by svo_hits_pack and unpacked by svo_hits_unpack on arrival."""
+
+    def __init__(self, args, rt, tree, dist, torch, gdev, W, H, STEPS, ppx, ppy, cam, origins, rank, world, counts, offs, n_mine, outs,
+                 nbuf):
+        self.a, self.rt, self.tree, self.dist, self.torch = args, rt, tree, dist, torch
+        self.W, self.H, self.world, self.rank = W, H, world, rank
+        self.counts, self.offs, self.n_mine = counts, offs, n_mine
+        self.nframes = len(origins)
+        self.nbuf = nbuf
+        self.wire = not args.shade
+        self.outs = outs
+        self.desc = None
+        # frames sent per destination rank: frame f -> rank f % world; receive my frames from every rank
+        self.mine = list(range(rank, self.nframes, world))
+        self.sends, self.recvs = [], []
+        for b in range(nbuf):
+            snd, rcv = [], []
+            if self.wire:
+                snd.append(torch.zeros((n_mine * self.nframes, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
+                rcv.append(torch.zeros((max(1, len(self.mine)) * W * H, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
+            if args.ao:
+                snd.append(outs[b]["ao"])
+                rcv.append(torch.zeros(max(1, len(self.mine)) * W * H, dtype=torch.uint8, device=gdev))
+            if args.shade:
+                snd.append(outs[b]["rgba"])
+                rcv.append(torch.zeros((max(1, len(self.mine)) * W * H, 4), dtype=torch.float32, device=gdev))
+            self.sends.append(snd)
+            self.recvs.append(rcv)
+        self.host = args.dist_backend != "nccl"
+        self.recv_host = [[torch.empty_like(x, device="cpu") for x in r] for r in self.recvs] if self.host else None
+        self.desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
+                                       frame_origins=origins if self.nframes > 1 else None)
+        self.src_descs = {f: [rt.Tree.frame_desc(origins[f], cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world)
+                              for r in range(world)] for f in self.mine}
+        self.frames = rt.Tree.alloc_hits(max(1, len(self.mine)) * W * H, gdev.index) if self.wire else None
+        self.pending = {}
+
+    def _splits(self, elems_per_record):
+        """all_to_all_single splits: my records of frame f go to rank f % N (frames in order); I receive
+        my frames' shards from every rank, frame by frame"""
+        send = [0] * self.world
+        for f in range(self.nframes):
+            send[f % self.world] += self.n_mine * elems_per_record
+        recv = [sum(self.counts[r] for _ in self.mine) * elems_per_record for r in range(self.world)]
+        return send, recv
+
+    def _order_send(self, x):
+        # records of frame f at f * n_mine: regroup by destination rank (frames f, f + N, ... per rank)
+        idx = [f for r in range(self.world) for f in range(r, self.nframes, self.world)]
+        if idx == list(range(self.nframes)):
+            return x
+        n = self.n_mine
+        return self.torch.cat([x[f * n:(f + 1) * n] for f in idx])
+
+    def step(self, k, b, stream):
+        torch, dist = self.torch, self.dist
+        with torch.cuda.stream(stream):
+            if self.wire:
+                self.tree.pack_hits(self.desc, self.outs[b], self.sends[b][0], stream)
+            works, keep = [], []
+            for i, (snd, rcv) in enumerate(zip(self.sends[b], self.recvs[b])):
+                s_split, r_split = self._splits(1)
+                src = self._order_send(snd)
+                src = src if not self.host else src.cpu()
+                dst = rcv if not self.host else self.recv_host[b][i]
+                dst = dst[:sum(r_split)]
+                works.append(dist.all_to_all_single(dst, src, output_split_sizes=r_split, input_split_sizes=s_split, async_op=True))
+                keep.append(src)
+            self.pending[k] = (works, keep, b)
+            if (k - 1) in self.pending:
+                self._unpack(k - 1, stream)
+        return None
+
+    def _unpack(self, k, stream):
+        works, _, b = self.pending.pop(k)
+        for w in works:
+            w.wait()
+        if self.host:
+            for i, h in enumerate(self.recv_host[b]):
+                self.recvs[b][i].copy_(h)
+        if not self.wire:
+            return
+        # received layout: from rank r, its shards of my frames in order
+        base = 0
+        for r in range(self.world):
+            for j, f in enumerate(self.mine):
+                lo = j * self.W * self.H + self.offs[r]
+                part = {key: v[lo:lo + self.counts[r]] for key, v in self.frames.items()}
+                self.tree.unpack_hits(self.src_descs[f][r], self.recvs[b][0][base:base + self.counts[r]], part, stream)
+                base += self.counts[r]
+
+    def drain(self, stream):
+        with self.torch.cuda.stream(stream):
+            for k in sorted(self.pending):
+                self._unpack(k, stream)
+
+    def verify(self, f, one):
+        """frame f (displayed here) reassembled from the shards == a one-GPU cast of it"""
+        from raytracing_test_amd import shard
+
+        j = self.mine.index(f)
+        got = self.rt.decode_hits({key: v[j * self.W * self.H:(j + 1) * self.W * self.H] for key, v in self.frames.items()})
+        ok = True
+        for r in range(self.world):
+            rows = shard.shard_pixel_rows(self.H, r, self.world)
+            idx = (rows[:, None] * self.W + np.arange(self.W)[None, :]).reshape(-1)
+            lo = self.offs[r]
+            ok &= all(np.array_equal(got[key][lo:lo + self.counts[r]], one[key][idx]) for key in ("pos", "steps", "hit", "axis", "material", "t"))
+        return ok
+
+
+def print_stats(rt, tree, d0, out, stream, torch):
+    nblk = rt.Tree.blocks(d0)
+    for mode in (rt.CAST_STATS, rt.CAST_TIMELINE):
+        st = torch.zeros(rt.STATS_HEADER + 2 * nblk + rt.Tree.count(d0), dtype=torch.int64, device=out["t"].device)
+        d0.flags |= mode
+        d0.stats = st.data_ptr()
+        tree.cast(d0, out, stream)
+        torch.cuda.synchronize()
+        d0.flags &= ~mode
+        allv = st.cpu().numpy()
+        if mode == rt.CAST_STATS:
+            vals = allv[:rt.STATS_HEADER]
+            if os.environ.get("SVO_RAY_WORK"):  # per-pixel lookups / brick steps for offline analysis
+                np.save(os.environ["SVO_RAY_WORK"], allv[rt.STATS_HEADER + 2 * nblk:])
+            per = [v / max(1, vals[0]) * (64 if k.startswith("wave_") and not k.endswith("_x64") else 1) for k, v in zip(rt.STAT_NAMES, vals)]
+            print("stats per ray (wave_* per wave): " + ", ".join("%s=%.3f" % (k, v) for k, v in zip(rt.STAT_NAMES, per)) +
+                  "; SIMD efficiency %.3f" % (vals[7] / max(1, vals[8])), file=sys.stderr)
+            continue
+        stamps = allv[rt.STATS_HEADER:rt.STATS_HEADER + 2 * nblk].reshape(-1, 2)
+        stamps = stamps[stamps[:, 1] > 0].astype(np.float64) / 100.0  # launched blocks; us (100 MHz)
+        t0s = stamps[:, 0].min()
+        dur = stamps[:, 1] - stamps[:, 0]
+        span = stamps[:, 1].max() - t0s
+        bins = np.linspace(0, span, 17)
+        res = [int(((stamps[:, 0] - t0s < b1) & (stamps[:, 1] - t0s > b0)).sum()) for b0, b1 in zip(bins[:-1], bins[1:])]
+        tenths = [float(np.mean(c)) for c in np.array_split(dur, 10)]
+        ends = np.sort(stamps[:, 1] - t0s)
+        print("timeline: span %.1f us, mean block %.1f us, max %.1f us, last 10%% of blocks end after %.1f us; blocks overlapping "
+              "each 1/16 of the span %s; mean block us per tenth of the grid %s"
+              % (span, dur.mean(), dur.max(), ends[int(len(ends) * 0.9)], res, ["%.0f" % x for x in tenths]), file=sys.stderr)
 
 
 if __name__ == "__main__":

@@ -29,6 +29,14 @@ def main():
     e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, nthreads=8) / (1920 * 1080)
     res["C3"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
                  "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
+    # C4: §8(d) "for AO: add <= 5 steps x E per sample" -- the AO rays' node entries (each continues the
+    # restart model from the primary's final lookup), 16 + 4 B per entry, per primary ray of the frame;
+    # B_OUT grows by the 1-B AO count
+    for n_ao in (16, 20):
+        ea = t.frame_entries_ao((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, n_ao, 5, nthreads=8) / (1920 * 1080)
+        res["C4_ao%d" % n_ao] = {"e_child_per_ray": e, "e_ao_per_ray": ea,
+                                 "bytes_per_ray": 16 * (e + 1) + 4 * e + 20 * ea + B_OUT + 1,
+                                 "tree": "as C3; AO %d samples x 5 steps per hit" % n_ao}
     # C5: 7 levels, 3840x2160 from the same pose; every ray lands within ~2,600 voxels of the camera,
     # so the oracle tree over the first 4096^2 columns of the 16384^2 terrain sees exactly the same
     # voxels (a full 16384^2 reference-format tree would exceed the 2^32-byte pools)
@@ -36,6 +44,11 @@ def main():
     e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 3840, 2160, 16384, nthreads=8) / (3840 * 2160)
     res["C5"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
                  "tree": "depth-14 (7 levels), first 4096^2 columns, reference node/array format, uniform regions collapsed"}
+    # C1: the dense 256^3 grid, "1 B per DDA step plus output" (§8d), reference camera, 256^2 rays, S = 300
+    D = O.Dense(ref, 256)
+    r = D.cast_frame((35, 50, 35), O.normalize((1, 0, 1)), 256, 256, 300)
+    st = r["dda_steps"] / (256 * 256)
+    res["C1"] = {"dda_steps_per_ray": st, "bytes_per_ray": st + B_OUT, "tree": "dense u8 grid of the reference world's [0,256)^3"}
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "profiles", "bray.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))

@@ -1022,7 +1022,17 @@ EXPORT int orc_cast_frame_dense(const odense* D, const float org[3], const float
  * lookup stopped) and descends; every descent is one 4 B child-slot read + one 16 B node read.
  * Returns the summed E_child over the rays of a frame (plus the frame's DDA step count).
  * ---------------------------------------------------------------------------------------------- */
-static uint64_t o_count_entries(const otree* t, const float org[3], const float dir[3], int steps) {
+typedef struct {
+    uint32_t stack[16];
+    int depth;   /* depth of the node where the previous lookup stopped */
+    int prev[3]; /* the previously looked-up voxel */
+    int have_prev;
+} o_estate;
+
+/* walk one ray (ray_caster.cpp:19-87 DDA) and count node entries under the restart model, continuing
+   from S (the lookup state a previous ray left); *hit / pos / last / axis describe where it ended */
+static uint64_t o_walk_entries(const otree* t, o_estate* S, const float org[3], const float dir[3], int steps, int* hit, int pos[3],
+                               int last[3], int* axis) {
     int L = t->max_depth - 1;
     int st[3];
     double dl[3], ad[3], ex[3], dp[3];
@@ -1036,59 +1046,96 @@ static uint64_t o_count_entries(const otree* t, const float org[3], const float 
         if (st[a] < 0) ex[a] -= 1;
     }
     for (int a = 0; a < 3; a++) dp[a] = ad[a] - (ex[a] - (double)r[a]) * dl[a];
-    uint32_t stack[16];
-    stack[0] = t->root;
-    int depth = 0; /* depth of the node where the previous lookup stopped */
-    int prev[3] = {r[0], r[1], r[2]};
-    int have_prev = 0;
     uint64_t entries = 0;
+    *hit = 0;
+    *axis = -1;
     while (steps--) {
         int ax;
         if (dp[0] < dp[1] && dp[0] < dp[2]) ax = 0;
         else if (dp[1] < dp[2]) ax = 1;
         else ax = 2;
+        memcpy(last, r, sizeof(r));
         r[ax] += st[ax];
         dp[ax] += ad[ax];
+        *axis = ax;
         /* common ancestor depth: number of leading levels whose 2-bit digits agree */
         int n = 0;
-        if (have_prev) {
+        if (S->have_prev) {
             for (n = 0; n < L; n++) {
                 int off = 2 * (L - 1 - n);
-                if (o_child_index(r[0], r[1], r[2], off) != o_child_index(prev[0], prev[1], prev[2], off)) break;
+                if (o_child_index(r[0], r[1], r[2], off) != o_child_index(S->prev[0], S->prev[1], S->prev[2], off)) break;
             }
         }
-        if (n < depth) depth = n;
+        if (n < S->depth) S->depth = n;
         /* descend from stack[depth] */
         uint32_t f = 0;
         uint64_t c = ~0ull;
         for (;;) {
-            const onode* nd = NODE(t, stack[depth]);
+            const onode* nd = NODE(t, S->stack[S->depth]);
             if (nd->flags & 1) {
                 f = nd->flags;
                 c = nd->w0;
                 break;
             }
-            if (depth >= L) break; /* corrupted (root-63 region): stop counting */
-            int off = 2 * (L - 1 - depth);
+            if (S->depth >= L) break; /* corrupted (root-63 region): stop counting */
+            int off = 2 * (L - 1 - S->depth);
             int idx = o_child_index(r[0], r[1], r[2], off);
             if (!((nd->w0 >> idx) & 1)) break;
-            stack[depth + 1] = ARR(t, nd->w1)->c[idx];
-            depth++;
+            S->stack[S->depth + 1] = ARR(t, nd->w1)->c[idx];
+            S->depth++;
             entries++;
         }
-        prev[0] = r[0];
-        prev[1] = r[1];
-        prev[2] = r[2];
-        have_prev = 1;
-        if (c != ~0ull && (f & 0x10) == 0) break;
+        memcpy(S->prev, r, sizeof(r));
+        S->have_prev = 1;
+        if (c != ~0ull && (f & 0x10) == 0) {
+            *hit = 1;
+            break;
+        }
     }
+    memcpy(pos, r, sizeof(r));
     return entries;
+}
+
+static uint64_t o_count_entries(const otree* t, const float org[3], const float dir[3], int steps) {
+    o_estate S;
+    memset(&S, 0, sizeof(S));
+    S.stack[0] = t->root;
+    int hit, pos[3], last[3], axis;
+    return o_walk_entries(t, &S, org, dir, steps, &hit, pos, last, &axis);
+}
+
+static inline void o_ao_dir(const float h[3], int ax, int sg, float d[3]);
+EXPORT void orc_hemisphere(int n, float* out);
+
+/* §8(d) "for AO: add <= 5 steps x E per sample": the node entries of a hit's AO rays (A8: from the
+   centre of lastPos, the table turned to the hit face), each continuing the restart model from the
+   lookup state the primary ray left (the shader-style stack of the hit voxel) */
+static uint64_t o_count_entries_ao(const otree* t, const float org[3], const float dir[3], int steps, const float* table, int n_ao,
+                                   int ao_steps) {
+    o_estate S;
+    memset(&S, 0, sizeof(S));
+    S.stack[0] = t->root;
+    int hit, pos[3], last[3], axis;
+    (void)o_walk_entries(t, &S, org, dir, steps, &hit, pos, last, &axis);
+    if (!hit || axis < 0) return 0;
+    int sg = last[axis] - pos[axis];
+    float o2[3] = {(float)last[0] + 0.5f, (float)last[1] + 0.5f, (float)last[2] + 0.5f};
+    uint64_t e = 0;
+    for (int i = 0; i < n_ao; i++) {
+        float d[3];
+        o_ao_dir(table + 3 * i, axis, sg, d);
+        o_estate A = S;
+        int h2, p2[3], l2[3], a2;
+        e += o_walk_entries(t, &A, o2, d, ao_steps, &h2, p2, l2, &a2);
+    }
+    return e;
 }
 
 typedef struct {
     const otree* t;
     float org[3], cam[3], ppx, ppy, rw, rh;
-    int W, H, steps, tid, nthreads;
+    int W, H, steps, tid, nthreads, n_ao, ao_steps;
+    const float* table;
     const int64_t* pix;
     int64_t n;
     uint64_t sum;
@@ -1100,13 +1147,17 @@ static void* o_entries_worker(void* p) {
         int64_t pi = j->pix ? j->pix[k] : k;
         float d[3];
         o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
-        s += o_count_entries(j->t, j->org, d, j->steps);
+        s += j->n_ao ? o_count_entries_ao(j->t, j->org, d, j->steps, j->table, j->n_ao, j->ao_steps)
+                     : o_count_entries(j->t, j->org, d, j->steps);
     }
     j->sum = s;
     return NULL;
 }
-EXPORT uint64_t orc_frame_entries(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
-                                  const int64_t* pix, int64_t n, int nthreads) {
+static uint64_t o_frame_entries(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
+                                int n_ao, int ao_steps, const int64_t* pix, int64_t n, int nthreads) {
+    float table[3 * 64];
+    if (n_ao > 64) n_ao = 64;
+    if (n_ao > 0) orc_hemisphere(n_ao, table);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -1119,6 +1170,7 @@ EXPORT uint64_t orc_frame_entries(const otree* t, const float org[3], const floa
         j->ppx = ppx; j->ppy = ppy;
         j->rw = 1.0f / (float)W; j->rh = 1.0f / (float)H;
         j->W = W; j->H = H; j->steps = steps;
+        j->n_ao = n_ao > 0 ? n_ao : 0; j->ao_steps = ao_steps; j->table = table;
         j->pix = pix;
         j->n = pix ? n : (int64_t)W * H;
         j->tid = i;
@@ -1132,6 +1184,15 @@ EXPORT uint64_t orc_frame_entries(const otree* t, const float org[3], const floa
     }
     free(jobs);
     return s;
+}
+EXPORT uint64_t orc_frame_entries(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
+                                  const int64_t* pix, int64_t n, int nthreads) {
+    return o_frame_entries(t, org, cam, ppx, ppy, W, H, steps, 0, 0, pix, n, nthreads);
+}
+/* the AO rays' entries only (summed over the frame's hits), see o_count_entries_ao */
+EXPORT uint64_t orc_frame_entries_ao(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H,
+                                     int steps, int n_ao, int ao_steps, const int64_t* pix, int64_t n, int nthreads) {
+    return o_frame_entries(t, org, cam, ppx, ppy, W, H, steps, n_ao, ao_steps, pix, n, nthreads);
 }
 
 /* FNV-1a digest of getBlock over a box (material identity = (flags, color)) */

@@ -118,6 +118,9 @@ def lib(native=False):
                                        vp, vp, vp, vp, C.POINTER(C.c_uint64)]
     L.orc_frame_entries.restype = C.c_uint64
     L.orc_frame_entries.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, vp, C.c_int64, C.c_int]
+    L.orc_frame_entries_ao.restype = C.c_uint64
+    L.orc_frame_entries_ao.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
+                                       C.c_int]
     L.orc_digest_box.restype = C.c_uint64
     L.orc_digest_box.argtypes = [vp] + [C.c_int] * 6
     L.orc_dump_box.argtypes = [vp] + [C.c_int] * 6 + [_u32p, _u64p]
@@ -316,6 +319,14 @@ class Tree:
         n = W * H if pixels is None else len(pixels)
         pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
         return self.L.orc_frame_entries(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, _ptr(pix), n, nthreads)
+
+    def frame_entries_ao(self, org, cam, W, H, steps, n_ao, ao_steps=5, ppx=None, ppy=None, pixels=None, nthreads=8):
+        """node entries of the hits' AO rays (restart model continued from each primary's final lookup)"""
+        if ppx is None:
+            ppx, ppy = proj_plane(W, H)
+        n = W * H if pixels is None else len(pixels)
+        pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
+        return self.L.orc_frame_entries_ao(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, n_ao, ao_steps, _ptr(pix), n, nthreads)
 
 
 class Dense:

@@ -1,20 +1,28 @@
 #!/bin/bash
-# One guarded evidence session (after the GPU parity suite has passed): bench lines for C3 (+ CPU
-# baseline), C4 (16 / 20 AO rays), C5 and the shading pass, a 2-rank gloo rehearsal of the N>1 path on
-# one GPU, the rocprofv3 kernel trace of the C3 bench, then the PMC passes (traffic, SQ).
-# usage: tools/evidence.sh <tag>
+# One guarded evidence session (after the GPU parity suite has passed): bench lines of every config
+# (C3 / C4 / C5 / C2 / shaded with their CPU baselines, C1), the single-rank C-ABI RCCL exchange, gloo
+# rehearsals of the N>1 paths on one GPU (weak, strong, AO, shaded), the rocprofv3 kernel trace of the
+# C3 bench.  usage: tools/evidence.sh <tag>
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-ev}; OUT=gpurun_out/$TAG; mkdir -p $OUT; export TMPDIR=/tmp
 step() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; "$@"; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
-step c3 timeout -k 10 300 bash -c "python bench.py > $OUT/bench.json 2> $OUT/bench.err"
-step c4_16 timeout -k 10 120 bash -c "python bench.py --ao 16 --no-cpu-baseline > $OUT/bench_c4_ao16.json 2>> $OUT/bench.err"
-step c4_20 timeout -k 10 120 bash -c "python bench.py --ao 20 --no-cpu-baseline > $OUT/bench_c4_ao20.json 2>> $OUT/bench.err"
-step c5 timeout -k 10 300 bash -c "python bench.py --config c5 > $OUT/bench_c5.json 2>> $OUT/bench.err"
-step c2 timeout -k 10 120 bash -c "python bench.py --config c2 --no-cpu-baseline > $OUT/bench_c2.json 2>> $OUT/bench.err"
-step c2cam0 timeout -k 10 120 bash -c "python bench.py --config c2cam0 --no-cpu-baseline > $OUT/bench_c2cam0.json 2>> $OUT/bench.err"
-step shade timeout -k 10 120 bash -c "python bench.py --shade --no-cpu-baseline > $OUT/bench_shade.json 2>> $OUT/bench.err"
-step gloo2 timeout -k 10 300 bash -c "python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 1 --dist-backend gloo --verify > $OUT/bench_gloo2.json 2> $OUT/gloo2.err"
+b() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python bench.py "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_$name.err; exit $rc; }; cut -c1-300 $OUT/bench_$name.json; }
+d() { local name=$1 n=$2 port=$3; shift 3; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --dist-backend gloo "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$name.err; exit $rc; }; grep '^{' $OUT/bench_$name.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['n_gpus'], d['scaling'], round(d['value']/1e6,1), 'M rays/s', 'verified', d.get('gather_verified'))"; }
+b c3
+b c1
+b c4_ao16 --ao 16
+b c4_ao20 --ao 20 --no-cpu-baseline
+b c5
+b c2
+b c2cam0 --no-cpu-baseline
+b shade --shade
+b xchg1 --force-exchange --verify --no-cpu-baseline
+b xchg1_ao --force-exchange --verify --no-cpu-baseline --ao 16
+b c5_xchg1 --config c5 --frames 1 --force-exchange --verify --no-cpu-baseline
+d g2 2 29541 --steps 4 --warmup 1 --verify
+d g2_strong 2 29542 --steps 4 --warmup 1 --frames 1 --verify
+d g3_f2 3 29543 --steps 4 --warmup 1 --frames 2 --verify
+d g2_ao 2 29544 --steps 4 --warmup 1 --ao 16 --verify
+d g2_shade 2 29545 --steps 4 --warmup 1 --shade
 step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/prof.err
-step pmc timeout -k 10 600 bash tools/pmc.sh ${TAG}_pmc
-step sq timeout -k 10 600 bash tools/pmc_sq.sh ${TAG}_sq

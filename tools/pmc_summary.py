@@ -31,8 +31,20 @@ def per_dispatch(d, kernel="k_cast"):
     return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
 
 
-def main(out):
-    res = {"kernel": "k_cast", "source": out}
+def bench_line(out):
+    """the bench JSON line of a pass (its rays per launch)"""
+    for f in sorted(glob.glob(os.path.join(out, "pmc_*.log"))):
+        for line in open(f):
+            if line.startswith("{"):
+                try:
+                    return json.loads(line)
+                except ValueError:
+                    pass
+    return None
+
+
+def main(out, bench_args=""):
+    res = {"kernel": "k_cast", "source": out, "bench_args": bench_args}
     counters = {}
     for d in sorted(glob.glob(os.path.join(out, "pmc_*")) + glob.glob(os.path.join(out, "sq_*"))):
         if os.path.isdir(d):
@@ -49,8 +61,18 @@ def main(out):
     h, m = counters.get("TCC_HIT_sum"), counters.get("TCC_MISS_sum")
     if h is not None and m is not None and h + m > 0:
         res["l2_hit_rate"] = h / (h + m)
+    b = bench_line(out)
+    if b and b.get("roofline"):
+        res["rays_per_launch"] = b["roofline"]["rays_per_launch"]
+        res["bench_avg_launch_ms"] = b["roofline"]["avg_launch_ms"]
+    elif counters.get("SQ_WAVES"):
+        res["rays_per_launch"] = counters["SQ_WAVES"] * 64  # one 64-lane wave per 16x4 footprint
+    if counters.get("SQ_WAVES") and counters.get("SQ_INSTS_VALU"):
+        res["valu_per_wave"] = counters["SQ_INSTS_VALU"] / counters["SQ_WAVES"]
+        if counters.get("SQ_INSTS_SALU"):
+            res["salu_per_wave"] = counters["SQ_INSTS_SALU"] / counters["SQ_WAVES"]
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "")
