@@ -10,12 +10,12 @@ step() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; "$@"; local 
 b() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python bench.py "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_$name.err; exit $rc; }; cut -c1-300 $OUT/bench_$name.json; }
 d() { local name=$1 n=$2 port=$3; shift 3; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --dist-backend gloo "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$name.err; exit $rc; }; grep '^{' $OUT/bench_$name.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['n_gpus'], d['scaling'], round(d['value']/1e6,1), 'M rays/s', 'verified', d.get('gather_verified'))"; }
 b c3
-b c1
+b c1 --config c1
 b c4_ao16 --ao 16
 b c4_ao20 --ao 20 --no-cpu-baseline
-b c5
-b c2
-b c2cam0 --no-cpu-baseline
+b c5 --config c5
+b c2 --config c2
+b c2cam0 --config c2cam0 --no-cpu-baseline
 b shade --shade
 b xchg1 --force-exchange --verify --no-cpu-baseline
 b xchg1_ao --force-exchange --verify --no-cpu-baseline --ao 16
