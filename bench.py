@@ -163,11 +163,12 @@ def cpu_baseline(args, cfg, ppx, ppy, gpu):
         what = "castRayFromCam over a dense u8 grid (getBlock seam ray_caster.cpp:81, coordinates & 255)"
     elif args.shade:
         sun = np.asarray(O.normalize((2.0, 1.0, 4.0)))
-        ref, dt = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt))
-        _, dt1 = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1))
+        ref, dt = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt, liquid=True))
+        _, dt1 = _timed(lambda: T.shade_frame(org, dn, W, H, S, sun, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1, liquid=True))
         if gpu is not None:
             parity = bool(np.abs(gpu["rgba"][pix] - ref).max() <= 2e-6)
-        what = "the shading pass (oracle orc_shade_frame: castRayFromCam + reflections + 75-step shadow ray)"
+        what = "the shading pass (oracle orc_shade_frame, liquid mode: castRayFromCam + reflections + refraction / tint by " \
+               "water and glass + 75-step shadow ray)"
     elif args.ao:
         (ao, hit), dt = _timed(lambda: T.cast_frame_ao(org, dn, W, H, S, args.ao, 5, ppx=ppx, ppy=ppy, pixels=pix, nthreads=nt))
         _, dt1 = _timed(lambda: T.cast_frame_ao(org, dn, W, H, S, args.ao, 5, ppx=ppx, ppy=ppy, pixels=pix1, nthreads=1))
@@ -336,6 +337,14 @@ def main():
     else:  # noise + build in HBM (identical arrays, tests/test_gpu_build.py); already uploaded
         tree = rt.Tree.terrain_gpu(cfg["levels"], cfg["cols"], cfg["cols"], dev)
         build_s = time.time() - t0
+    scene = None
+    if args.shade:  # the shading scene: every block, water included (it refracts, low_res.frag:214-229)
+        if args.config in ("c1", "c2", "c2cam0"):
+            scene = (rt.World.reference() if args.config != "c1" else w4).build(rt.VIEW_ALL).upload(dev)
+        elif args.host_build:
+            scene = rt.Tree.terrain(cfg["levels"], cfg["cols"], cfg["cols"], nthreads=16, view=rt.VIEW_ALL).upload(dev)
+        else:
+            scene = rt.Tree.terrain_gpu(cfg["levels"], cfg["cols"], cfg["cols"], dev, view=rt.VIEW_ALL)
     info = tree.info()
     ppx, ppy = rt.proj_plane(W, H)
     cam = rt.normalize(cfg["cam"])
@@ -404,7 +413,7 @@ def main():
             if ev is not None:
                 ev[0].record(stream)
             if args.shade:
-                tree.shade(desc, outs[b]["rgba"], out=outs[b], stream=stream)
+                tree.shade(desc, outs[b]["rgba"], out=outs[b], stream=stream, scene=scene)
             else:
                 tree.cast(desc, outs[b], stream)
             if ev is not None:
@@ -495,12 +504,12 @@ def main():
             gpu = rt.decode_hits(outs[0])
         cpu = cpu_baseline(args, cfg, ppx, ppy, gpu)
     work = ("C4 (C3 + %d hemisphere AO rays per hit, 5 steps each): " % args.ao if args.ao else "") + \
-           ("shaded (low_res.frag colour model, 75-step shadow rays): " if args.shade else "")
+           ("shaded (low_res.frag colour model, water refracts (SVO_VIEW_ALL scene), 75-step shadow rays): " if args.shade else "")
     metric = cfg["metric"]
     if args.ao:
         metric = "primary rays/sec at 1080p with %d-sample hemisphere AO per hit, depth-12 SVO (config 4); achieved HBM GB/s vs roofline" % args.ao
     if args.shade:
-        metric = "shaded primary rays/sec (reflections + sun shadow ray)"
+        metric = "shaded primary rays/sec (reflections, refraction by water, sun shadow ray)"
     line = {
         "metric": metric,
         "value": round(value, 1),
@@ -527,7 +536,7 @@ def main():
                        ("torch.distributed all_to_all_single: " + ("rgba image" if args.shade else "12-B wire hit records") +
                         ", frame f to rank f %% N" + ("; " + xnote if xnote else ""))),
                    "tree_nodes": info.n_nodes, "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
-                   "tree_builder": builder},
+                   "tree_builder": builder, **({"scene_nodes": scene.info().n_nodes} if scene is not None else {})},
         "roofline": roof,
         "cpu_baseline": cpu,
         **({"gather_verified": verified} if verified is not None else {}),

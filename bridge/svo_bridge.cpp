@@ -11,7 +11,8 @@
 
 namespace {
 svo_world* g_world = nullptr;
-svo_tree* g_tree = nullptr;
+svo_tree* g_tree = nullptr;   // solid view: castRayFromCam, primary frames, shadow rays
+svo_tree* g_scene = nullptr;  // full view (water stored): what the shaded frame's rays walk (low_res.frag)
 bool g_rebuild = true;  // the world changed without a tree to patch (genWorld, edits before the first upload)
 
 void check(int rc, const char* what) {
@@ -31,6 +32,13 @@ void edited(const Pos& p, int level) {
     }
     const int32_t xyz[3] = {p.x, p.y, p.z};
     check(svo_tree_update(g_tree, g_world, xyz, 1, level), "svo_tree_update");
+    check(svo_tree_update(g_scene, g_world, xyz, 1, level), "svo_tree_update");
+}
+
+void drop_trees() {
+    if (g_tree) svo_tree_destroy(g_tree);
+    if (g_scene) svo_tree_destroy(g_scene);
+    g_tree = g_scene = nullptr;
 }
 
 void camera(float o[3], float d[3]) {
@@ -45,9 +53,8 @@ void camera(float o[3], float d[3]) {
 
 // tetrahexa_tree.cpp:13-41 (maxDepth 6 = 5 levels, tetrahexa_tree.hpp:6)
 void initTetraHexaTree() {
-    if (g_tree) svo_tree_destroy(g_tree);
+    drop_trees();
     if (g_world) svo_world_destroy(g_world);
-    g_tree = nullptr;
     check(svo_world_create(maxDepth - 1, &g_world), "svo_world_create");
     check(svo_init_tetra_hexa_tree(g_world), "svo_init_tetra_hexa_tree");
     g_rebuild = true;
@@ -56,8 +63,7 @@ void initTetraHexaTree() {
 // world_gen.cpp:13-42 (200 x 200 columns)
 void genWorld() {
     check(svo_gen_world(g_world, 200, 200), "svo_gen_world");
-    if (g_tree) svo_tree_destroy(g_tree);
-    g_tree = nullptr;
+    drop_trees();
     g_rebuild = true;
 }
 
@@ -97,14 +103,16 @@ void traverseTree(Pos* pos, int count) {
 // genWorld) builds and uploads the tree; later calls upload only what edits changed
 void updateSsboData() {
     if (g_rebuild || !g_tree) {
-        if (g_tree) svo_tree_destroy(g_tree);
-        g_tree = nullptr;
+        drop_trees();
         check(svo_build(g_world, &g_tree), "svo_build");
         check(svo_upload(g_tree, 0), "svo_upload");
+        check(svo_build_view(g_world, SVO_VIEW_ALL, &g_scene), "svo_build_view");
+        check(svo_upload(g_scene, 0), "svo_upload");
         g_rebuild = false;
         return;
     }
     check(svo_tree_sync(g_tree), "svo_tree_sync");
+    check(svo_tree_sync(g_scene), "svo_tree_sync");
 }
 
 svo_tree* svoTree() { return g_tree; }
@@ -140,7 +148,7 @@ void svoCastPrimaryRays(int32_t width, int32_t height, int32_t steps, int32_t* p
     check(svo_cast_rays(g_tree, &d, &h, stream), "svo_cast_rays");
 }
 
-void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream) {
+void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream, float time) {
     if (!g_tree) updateSsboData();
     const svo_cast_desc d = frame_desc(width, height, 300);  // low_res.frag:310
     const RayResult look = RAY_CASTER::castRayFromCam(30);    // main.cpp:81, the lookingAtBlock uniform (:89)
@@ -153,5 +161,7 @@ void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t str
     sd.look_at[2] = look.pos.z;
     sd.look_at_valid = 1;
     sd.shadow_steps = 75;  // low_res.frag:382
+    sd.scene = g_scene;    // water refracts and tints (low_res.frag:214-229)
+    sd.time = time;        // the deltaTime uniform
     check(svo_shade_rays(g_tree, &d, &sd, rgba, nullptr, stream), "svo_shade_rays");
 }

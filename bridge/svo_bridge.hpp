@@ -23,7 +23,8 @@ void updateSsboData();
 // castRayFromCam-semantics primary ray per pixel of the camera's width x height frame into caller-owned
 // device buffers (24 B per pixel, include/svo_rt.h svo_hits), asynchronously on `stream`
 void svoCastPrimaryRays(int32_t width, int32_t height, int32_t steps, int32_t* pos_steps, float* t, uint32_t* info, hipStream_t stream);
-// the same frame shaded (low_res.frag's colour model, svo_shade_rays): one float4 per pixel
-void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream);
+// the same frame shaded (low_res.frag's colour model, svo_shade_rays, water refracting through the
+// full-view scene the shim keeps beside the solid tree): one float4 per pixel; time = deltaTime
+void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream, float time = 0.0f);
 // the tree the shim keeps in HBM (for direct use of the C ABI, e.g. svo_exchange_frames)
 svo_tree* svoTree();

@@ -23,7 +23,8 @@
 extern "C" {
 #endif
 
-#define SVO_RT_VERSION 3  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing */
+#define SVO_RT_VERSION 4  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
+                             4: tree views (liquid stored for the shading pass), svo_shade_desc.scene / time */
 
 enum {
     SVO_OK = 0,
@@ -99,14 +100,24 @@ typedef struct {
     uint64_t nodes_per_level[8];  /* nodes at depth 0..levels-1 */
     uint64_t device_bytes;        /* HBM footprint after svo_upload (0 before) */
     int32_t device;               /* -1 before svo_upload */
+    int32_t view;                 /* SVO_VIEW_SOLID / SVO_VIEW_ALL */
 } svo_tree_info;
+
+/* Tree views.  SVO_VIEW_SOLID (every cast): the blocks castRayFromCam hits (ray_caster.cpp:82) —
+   empty and LIQUID blocks are empty.  SVO_VIEW_ALL (the scene of the shading pass,
+   svo_shade_desc.scene): every stored block, liquid included, as low_res.frag's getBlock sees it. */
+#define SVO_VIEW_SOLID 0
+#define SVO_VIEW_ALL 1
 
 /* Linearise a world: collapse uniform regions, drop non-solid (empty / LIQUID) voxels, emit the
    breadth-first node array + material bytes + palette. */
 int svo_build(const svo_world* w, svo_tree** out);
+/* the same for a view (svo_build = SVO_VIEW_SOLID); edits (svo_tree_update) keep the tree's view */
+int svo_build_view(const svo_world* w, int32_t view, svo_tree** out);
 /* Build the same tree straight from genWorld's column formula over width x length columns
    (no per-voxel putBlock: depth-12 / depth-14 terrain); nthreads host threads (0 = all). */
 int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out);
+int svo_build_terrain_view(int32_t levels, int32_t width, int32_t length, int32_t nthreads, int32_t view, svo_tree** out);
 /* the same builder from caller-given column tops heights[x*length + z] (0 <= h <= extent-2) */
 int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t nthreads,
                           svo_tree** out);
@@ -115,6 +126,7 @@ int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const i
    node / material arrays equal svo_build_terrain's byte for byte; the tree comes back already
    uploaded to `device` (plus its host image). */
 int svo_build_terrain_gpu(int32_t levels, int32_t width, int32_t length, int32_t device, svo_tree** out);
+int svo_build_terrain_gpu_view(int32_t levels, int32_t width, int32_t length, int32_t device, int32_t view, svo_tree** out);
 int svo_build_heightfield_gpu(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t device, svo_tree** out);
 int svo_tree_get_info(const svo_tree* t, svo_tree_info* out);
 /* palette entry `id` (id 0 = empty block) */
@@ -286,16 +298,22 @@ int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo_cast_desc*
      look_at voxel   -> colour x 2 + 0.3 (:340-343)
    A block with flags & 7 == 3 reflects the ray while budget remains (:170-189, :319-331):
    the last crossing on the hit axis is undone, that axis's step and direction flip, the DDA
-   continues; finalColorMod *= 0.94 per reflection.  A refractive solid (flags & 7 == 5, not
-   liquid) while budget remains is passed with finalColorMod *= 0.95; the first one bends the ray
-   (refractRay :196-240, n 1.0 -> 1.1, normal = hit axis x step, the shader's origin-based exact
-   position) and deltaPos restarts from the current cell.  Liquid passes unbent (it is empty in
-   castRayFromCam and in the tree).  Single precision in the shader's operation order. */
+   continues; finalColorMod *= 0.94 per reflection.  A refractive block (flags & 7 == 5) while
+   budget remains is passed with finalColorMod *= (0.94, 0.97, 1.0) for liquid, 0.95 otherwise
+   (:214); the first one bends the ray (refractRay :196-240, n 1.0 -> 1.1, normal = hit axis x step,
+   for liquid plus the shader's wobble sin((time + exact.x * 0.2 - exact.z * 0.1) * 10) * 0.2 on x
+   and renormalised, :225-229; the shader's origin-based exact position) and deltaPos restarts from
+   the current cell.  Liquid is seen only through a scene tree of SVO_VIEW_ALL (built from the same
+   world or terrain as t); without one (scene == NULL) liquid passes unbent, as in castRayFromCam.
+   Single precision in the shader's operation order; sin through double precision, rounded once. */
 typedef struct {
     float sun_dir[3];      /* normalised sunDir (globals.cpp:23: normalize(2,1,4)) */
     int32_t look_at[3];    /* lookingAtBlock (main.cpp:81,89) */
     int32_t look_at_valid; /* 0: no highlight */
     int32_t shadow_steps;  /* 75 (low_res.frag:382) */
+    const svo_tree* scene; /* SVO_VIEW_ALL tree the primary / reflected / refracted ray walks (NULL: t);
+                              shadow rays walk t (liquid passes) */
+    float time;            /* deltaTime uniform of the liquid wobble (low_res.frag:226) */
 } svo_shade_desc;
 
 /* asynchronous on hip_stream; rgba: device float4 per ray; hits: optional hit records (may be NULL) */

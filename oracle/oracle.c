@@ -1330,12 +1330,11 @@ EXPORT void orc_cast_frame_ao(const otree* t, const float org[3], const float ca
  * colour model (genSkyBox :157-168, calcLightIntensity :242-252, shadow ray :373-391, highlight
  * :340-343, reflectRay :170-189, refractRay :196-240 for non-liquid blocks) over castRayFromCam hits.  Single precision, shader op order.
  * ---------------------------------------------------------------------------------------------- */
-/* refractRay(vec3, vec3, float, float) (:196-209) with n1 = 1.0, n2 = 1.1 and normal = the hit
-   axis times its step (:222-223); dot as ((x + y) + z), no fused operations. */
-static void o_refract_dir(float d[3], int ax, int st_ax) {
+/* refractRay(vec3, vec3, float, float) (:196-209) with n1 = 1.0, n2 = 1.1; dot as ((x + y) + z),
+   no fused operations. */
+static void o_refract_dir(float d[3], const float nin[3]) {
     const float r = 1.0f / 1.1f;
-    float n[3] = {0.0f, 0.0f, 0.0f};
-    n[ax] = (float)st_ax;
+    float n[3] = {nin[0], nin[1], nin[2]};
     float c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
     if (c1 < 0.0f) {
         for (int a = 0; a < 3; a++) n[a] = -n[a];
@@ -1346,6 +1345,24 @@ static void o_refract_dir(float d[3], int ax, int st_ax) {
     for (int a = 0; a < 3; a++) d[a] = r * d[a] + k * n[a];
 }
 
+/* GLSL sin for the liquid wobble (:226): defined here (and in the product, svo_common.h sin_f32)
+   as sin evaluated in double and rounded once to float — Cody-Waite reduction by pi/2, Taylor
+   polynomials on [-pi/4, pi/4] — the same double operations on both sides (no contraction). */
+static float o_sin_f32(float xf) {
+    const double x = (double)xf;
+    const double k = rint(x * 0.63661977236758134308);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double r2 = r * r;
+    const double sn = r + (r * r2) * (-1.6666666666666666e-01 + r2 * (8.3333333333333332e-03 + r2 * (-1.9841269841269841e-04 +
+                                     r2 * (2.7557319223985893e-06 + r2 * (-2.5052108385441720e-08 + r2 * 1.6059043836821613e-10)))));
+    const double cs = 1.0 + r2 * (-0.5 + r2 * (4.1666666666666664e-02 + r2 * (-1.3888888888888889e-03 + r2 * (2.4801587301587302e-05 +
+                                  r2 * (-2.7557319223985888e-07 + r2 * (2.0876756987868100e-09 + r2 * -1.1470745597729725e-11))))));
+    const int64_t q = (int64_t)k & 3;
+    const double v = (q & 1) ? cs : sn;
+    return (float)((q & 2) ? -v : v);
+}
+EXPORT float orc_sin_f32(float x) { return o_sin_f32(x); }
+
 /* o_cast with reflections and refractions.  A hit on a block with (flags & 7) == 3 while steps
    remain undoes the last crossing on the hit axis, flips that axis's step and direction, and
    continues (reflectRay :170-189).  A hit on a non-liquid block with (flags & 7) == 5 (liquid is
@@ -1353,10 +1370,14 @@ static void o_refract_dir(float d[3], int ax, int st_ax) {
    bends the ray (refractRay :211-240): the origin-based exact position (never advanced by the DDA,
    as in the shader) gets +1 on the other axes with a negative step, the direction is refracted, the
    ray rebuilt (A1), exact += min(step, 0) and deltaPos = absDelta - (exact - round) * delta from
-   the current cell.  *mod = finalColorMod (0.94 per reflection, 0.95 per refractive block, in
-   order). */
+   the current cell.  mod = finalColorMod (0.94 per reflection, 0.95 per refractive block, in
+   order).  liquid != 0: liquid blocks are not empty but blocks like any other (low_res.frag's
+   getBlock, :312-333): refractive liquid (flags & 7 == 5, the terrain's water 0x15) tints by
+   (0.94, 0.97, 1.0) (:214) and, when it is the first refractive block, bends the ray with the
+   normal's wobble x += sin((time + exact.x * 0.2 - exact.z * 0.1) * 10) * 0.2, renormalised
+   (:225-229; exact as float). */
 static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3], const float dir_in[3], int steps, orayres* R,
-                        float dir[3], int* nrefl, float* mod) {
+                        float dir[3], int* nrefl, float mod[3], int liquid, float time) {
     int st[3];
     double dl[3], ad[3], ex[3], dp[3];
     int r[3], last[3];
@@ -1374,7 +1395,7 @@ static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3],
     memset(R, 0, sizeof(*R));
     R->axis = -1;
     *nrefl = 0;
-    *mod = 1.0f;
+    mod[0] = mod[1] = mod[2] = 1.0f;
     for (int a = 0; a < 3; a++) last[a] = r[a];
     while (steps--) {
         int ax;
@@ -1393,22 +1414,32 @@ static void o_cast_refl(o_getblock_fn gb, const void* world, const float org[3],
             R->err = 1;
             break;
         }
-        if (c != ~0ull && (f & 0x10) == 0) {
+        const int liq = (f & 0x10) != 0;
+        if (c != ~0ull && (liquid || !liq)) {
             if ((f & 7u) == 3u && steps > 0) {
                 dp[ax] -= ad[ax];
                 st[ax] = -st[ax];
                 dir[ax] = -dir[ax];
                 (*nrefl)++;
-                *mod *= 0.94f;
+                for (int k = 0; k < 3; k++) mod[k] *= 0.94f;
                 continue;
             }
             if ((f & 7u) == 5u && steps > 0) {
-                *mod *= 0.95f;
+                mod[0] *= liq ? 0.94f : 0.95f;
+                mod[1] *= liq ? 0.97f : 0.95f;
+                mod[2] *= liq ? 1.0f : 0.95f;
                 if (!bent) {
                     bent = 1;
                     for (int a = 0; a < 3; a++)
                         if (a != ax && st[a] < 0) ex[a] += 1;
-                    o_refract_dir(dir, ax, st[ax]);
+                    float nrm[3] = {0.0f, 0.0f, 0.0f};
+                    nrm[ax] = (float)st[ax];
+                    if (liq) {
+                        const float arg = ((time + (float)ex[0] * 0.2f) - (float)ex[2] * 0.1f) * 10.0f;
+                        nrm[0] += o_sin_f32(arg) * 0.2f;
+                        o_normalize(nrm, nrm);
+                    }
+                    o_refract_dir(dir, nrm);
                     for (int a = 0; a < 3; a++) {
                         st[a] = dir[a] < 0 ? -1 : 1;
                         dl[a] = (double)(1.0f / dir[a]);
@@ -1463,12 +1494,12 @@ static void o_sky(const float d[3], const float sun[3], float o[3]) {
 }
 
 static void o_shade(o_getblock_fn gb, const void* world, const float org[3], const float d0[3], int steps, const float sun[3],
-                    const int32_t* look, int shadow_steps, float out[4]) {
+                    const int32_t* look, int shadow_steps, int liquid, float time, float out[4]) {
     orayres R;
     float dir[3];
     int nrefl;
-    float m;
-    o_cast_refl(gb, world, org, d0, steps, &R, dir, &nrefl, &m);
+    float m[3];
+    o_cast_refl(gb, world, org, d0, steps, &R, dir, &nrefl, m, liquid, time);
     float c[3];
     if (look && R.pos[0] == look[0] && R.pos[1] == look[1] && R.pos[2] == look[2]) {
         float b[3];
@@ -1477,7 +1508,7 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
     } else if (!R.hit) {
         float sk[3];
         o_sky(dir, sun, sk);
-        for (int k = 0; k < 3; k++) c[k] = sk[k] * m;
+        for (int k = 0; k < 3; k++) c[k] = sk[k] * m[k];
     } else {
         float col[3];
         o_color(R.color, col);
@@ -1486,7 +1517,7 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
         float l = sun[ax] * (float)(-sg);
         int facing = l > 0.0f;
         float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
-        for (int k = 0; k < 3; k++) c[k] = col[k] * inten * m;
+        for (int k = 0; k < 3; k++) c[k] = col[k] * inten * m[k];
         int dark = 0;
         if (nrefl == 0) {
             if (!facing) {
@@ -1499,7 +1530,7 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
             }
         }
         if (dark)
-            for (int k = 0; k < 3; k++) c[k] = col[k] * 0.3f * m;
+            for (int k = 0; k < 3; k++) c[k] = col[k] * 0.3f * m[k];
     }
     out[0] = c[0];
     out[1] = c[1];
@@ -1509,8 +1540,8 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
 
 typedef struct {
     const otree* t;
-    float org[3], cam[3], ppx, ppy, rw, rh, sun[3];
-    int W, H, steps, shadow_steps, tid, nthreads;
+    float org[3], cam[3], ppx, ppy, rw, rh, sun[3], time;
+    int W, H, steps, shadow_steps, tid, nthreads, liquid;
     const int32_t* look;
     const int64_t* pix;
     int64_t n;
@@ -1522,13 +1553,13 @@ static void* o_shade_worker(void* p) {
         int64_t pi = j->pix ? j->pix[k] : k;
         float d[3];
         o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
-        o_shade(o_gb_tree, j->t, j->org, d, j->steps, j->sun, j->look, j->shadow_steps, j->rgba + 4 * k);
+        o_shade(o_gb_tree, j->t, j->org, d, j->steps, j->sun, j->look, j->shadow_steps, j->liquid, j->time, j->rgba + 4 * k);
     }
     return NULL;
 }
 EXPORT void orc_shade_frame(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
                             const float sun[3], const int32_t* look, int shadow_steps, const int64_t* pix, int64_t n, int nthreads,
-                            float* rgba) {
+                            float* rgba, int liquid, float time) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -1543,6 +1574,8 @@ EXPORT void orc_shade_frame(const otree* t, const float org[3], const float cam[
         j->rw = 1.0f / (float)W; j->rh = 1.0f / (float)H;
         j->W = W; j->H = H; j->steps = steps; j->shadow_steps = shadow_steps;
         j->look = look;
+        j->liquid = liquid;
+        j->time = time;
         j->pix = pix;
         j->n = pix ? n : (int64_t)W * H;
         j->tid = i; j->nthreads = nthreads;

@@ -128,7 +128,9 @@ def lib(native=False):
     L.orc_cast_frame_ao.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, vp, C.c_int64,
                                     C.c_int, vp, vp]
     L.orc_shade_frame.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, _f32p, vp, C.c_int, vp, C.c_int64,
-                                  C.c_int, vp]
+                                  C.c_int, vp, C.c_int, C.c_float]
+    L.orc_sin_f32.restype = C.c_float
+    L.orc_sin_f32.argtypes = [C.c_float]
     _libs[path] = L
     return L
 
@@ -163,6 +165,10 @@ def hemisphere(n):
     out = np.zeros(3 * n, np.float32)
     lib().orc_hemisphere(n, out)
     return out.reshape(n, 3)
+
+
+def sin_f32(x):
+    return lib().orc_sin_f32(x)
 
 
 def noise2(seed, x, y):
@@ -301,8 +307,10 @@ class Tree:
                                  _ptr(hit))
         return ao, hit
 
-    def shade_frame(self, org, cam, W, H, steps, sun, look_at=None, shadow_steps=75, ppx=None, ppy=None, pixels=None, nthreads=8):
-        """shaded frame (svo_shade_rays contract, oracle.c §shading): (n, 4) float32 rgba in pixel order"""
+    def shade_frame(self, org, cam, W, H, steps, sun, look_at=None, shadow_steps=75, ppx=None, ppy=None, pixels=None, nthreads=8,
+                    liquid=False, time=0.0):
+        """shaded frame (svo_shade_rays contract, oracle.c §shading): (n, 4) float32 rgba in pixel order;
+        liquid: water refracts and tints as in low_res.frag (the product's SVO_VIEW_ALL scene)"""
         if ppx is None:
             ppx, ppy = proj_plane(W, H)
         n = W * H if pixels is None else len(pixels)
@@ -310,7 +318,7 @@ class Tree:
         look = None if look_at is None else np.ascontiguousarray(look_at, dtype=np.int32)
         rgba = np.zeros((n, 4), np.float32)
         self.L.orc_shade_frame(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, f3(sun), _ptr(look), shadow_steps, _ptr(pix), n, nthreads,
-                               _ptr(rgba))
+                               _ptr(rgba), 1 if liquid else 0, time)
         return rgba
 
     def frame_entries(self, org, cam, W, H, steps, ppx=None, ppy=None, pixels=None, nthreads=8):

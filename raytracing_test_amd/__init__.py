@@ -49,6 +49,7 @@ STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "bric
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: one hit record in the exchange format (svo_hits_pack)
+VIEW_SOLID, VIEW_ALL = 0, 1  # SVO_VIEW_*: castRayFromCam's blocks / every stored block (the shading scene)
 
 
 class SvoError(RuntimeError):
@@ -83,6 +84,7 @@ class TreeInfo(C.Structure):
         ("nodes_per_level", C.c_uint64 * 8),
         ("device_bytes", C.c_uint64),
         ("device", C.c_int32),
+        ("view", C.c_int32),
     ]
 
 
@@ -114,7 +116,8 @@ class Hits(C.Structure):
 
 
 class ShadeDesc(C.Structure):
-    _fields_ = [("sun_dir", C.c_float * 3), ("look_at", C.c_int32 * 3), ("look_at_valid", C.c_int32), ("shadow_steps", C.c_int32)]
+    _fields_ = [("sun_dir", C.c_float * 3), ("look_at", C.c_int32 * 3), ("look_at_valid", C.c_int32), ("shadow_steps", C.c_int32),
+                ("scene", C.c_void_p), ("time", C.c_float)]
 
 
 # globals.cpp:23: sun = normalize(vec3(2, 1, 4))
@@ -134,7 +137,7 @@ ABI_SYMBOLS = (
     "svo_build_heightfield", "svo_shade_rays", "svo_tree_update", "svo_tree_sync",
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
-    "svo_exchange_frames",
+    "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
 )
 
 
@@ -166,6 +169,9 @@ def lib():
     L.svo_gen_world.argtypes = [vp, i32, i32]
     L.svo_world_node_count.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.svo_build.argtypes = [vp, C.POINTER(vp)]
+    L.svo_build_view.argtypes = [vp, i32, C.POINTER(vp)]
+    L.svo_build_terrain_view.argtypes = [i32, i32, i32, i32, i32, C.POINTER(vp)]
+    L.svo_build_terrain_gpu_view.argtypes = [i32, i32, i32, i32, i32, C.POINTER(vp)]
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
     L.svo_tree_get_info.argtypes = [vp, C.POINTER(TreeInfo)]
     L.svo_tree_palette.argtypes = [vp, C.c_uint32, C.POINTER(Block)]
@@ -351,9 +357,10 @@ class World:
         _check(lib().svo_world_node_count(self._h, C.byref(n)), "svo_world_node_count")
         return n.value
 
-    def build(self):
+    def build(self, view=VIEW_SOLID):
+        """the linearised tree of this world: VIEW_SOLID for casts, VIEW_ALL (liquid stored) as a shading scene"""
         h = C.c_void_p()
-        _check(lib().svo_build(self._h, C.byref(h)), "svo_build")
+        _check(lib().svo_build_view(self._h, view, C.byref(h)), "svo_build_view")
         return Tree(h)
 
 
@@ -376,10 +383,10 @@ class Tree:
             self._h = None
 
     @classmethod
-    def terrain(cls, levels, width, length, nthreads=0):
+    def terrain(cls, levels, width, length, nthreads=0, view=VIEW_SOLID):
         """genWorld's column formula over width x length columns, built without per-voxel putBlock."""
         h = C.c_void_p()
-        _check(lib().svo_build_terrain(levels, width, length, nthreads, C.byref(h)), "svo_build_terrain")
+        _check(lib().svo_build_terrain_view(levels, width, length, nthreads, view, C.byref(h)), "svo_build_terrain_view")
         return cls(h)
 
     @classmethod
@@ -392,10 +399,10 @@ class Tree:
         return cls(t)
 
     @classmethod
-    def terrain_gpu(cls, levels, width, length, device=0):
+    def terrain_gpu(cls, levels, width, length, device=0, view=VIEW_SOLID):
         """svo_build_terrain on the GPU (noise + build in HBM): the tree comes back uploaded to `device`."""
         h = C.c_void_p()
-        _check(lib().svo_build_terrain_gpu(levels, width, length, device, C.byref(h)), "svo_build_terrain_gpu")
+        _check(lib().svo_build_terrain_gpu_view(levels, width, length, device, view, C.byref(h)), "svo_build_terrain_gpu_view")
         return cls(h)
 
     @classmethod
@@ -565,9 +572,12 @@ class Tree:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return out
 
-    def shade(self, desc, rgba, sun=None, look_at=None, shadow_steps=75, out=None, stream=None):
-        """Launch the shading pass (svo_shade_rays) for `desc`: rgba is a (n, 4) float32 device tensor."""
+    def shade(self, desc, rgba, sun=None, look_at=None, shadow_steps=75, out=None, stream=None, scene=None, time=0.0):
+        """Launch the shading pass (svo_shade_rays) for `desc`: rgba is a (n, 4) float32 device tensor.
+        scene: a VIEW_ALL Tree of the same world (liquid refracts and tints); time: the wobble's deltaTime."""
         sd = ShadeDesc()
+        sd.scene = scene._h if scene is not None else None
+        sd.time = time
         sd.sun_dir[:] = [float(x) for x in (sun if sun is not None else sun_dir())]
         if look_at is not None:
             sd.look_at[:] = [int(x) for x in look_at]
@@ -581,7 +591,7 @@ class Tree:
                                     C.c_void_p(s) if s else None), "svo_shade_rays")
 
     def shade_frame(self, origin, cam_dir, width, height, steps=300, sun=None, look_at=None, shadow_steps=75, ppx=None, ppy=None,
-                    tile_row_start=0, tile_row_step=1, with_hits=False, stream=None, sync=True, flags=0):
+                    tile_row_start=0, tile_row_step=1, with_hits=False, stream=None, sync=True, flags=0, scene=None, time=0.0):
         """One shaded frame: (n, 4) float32 rgba in hit-record order (and the hit records with with_hits)."""
         torch = _torch()
         d = self.frame_desc(origin, cam_dir, width, height, steps, ppx, ppy, tile_row_start, tile_row_step, flags, 0, 5)
@@ -589,7 +599,7 @@ class Tree:
         dev = self.info().device
         rgba = torch.empty((n, 4), dtype=torch.float32, device=torch.device("cuda", dev))
         out = self.alloc_hits(n, dev) if with_hits else None
-        self.shade(d, rgba, sun, look_at, shadow_steps, out, stream)
+        self.shade(d, rgba, sun, look_at, shadow_steps, out, stream, scene=scene, time=time)
         if sync:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return (rgba, out) if with_hits else rgba

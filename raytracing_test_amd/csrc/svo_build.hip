@@ -38,6 +38,7 @@ struct DevTerrain {
     const int16_t* hmax[kMaxPyr];
     int32_t dimz[kMaxPyr];
     uint32_t id_of[5];
+    int32_t view;  // SVO_VIEW_SOLID / SVO_VIEW_ALL
 };
 
 struct Region {
@@ -56,18 +57,9 @@ __device__ uint32_t g_classify(const DevTerrain& T, int32_t x0, int32_t y0, int3
     const bool partial = (x0 + s > T.W) || (z0 + s > T.L);
     const size_t ci = (size_t)(x0 >> (2 * k)) * T.dimz[k] + (z0 >> (2 * k));
     const int32_t hmin = T.hmin[k][ci], hmax = T.hmax[k][ci];
-    if (y1 < 1 || y0 > hmax) return G_EMPTY;
+    if (terrain_region_empty(T.view, hmax, y0, y1)) return G_EMPTY;
     if (partial) return G_MIXED;
-    if (y0 >= 1 && y1 <= hmin - 4) return T.id_of[TM_STONE];
-    if (hmin != hmax) return G_MIXED;
-    const int32_t h = hmin;
-    const uint32_t c0 = g_solid_class(T, h, y0);
-    const int32_t cand[4] = {1, h - 3, h, h + 1};
-    for (int i = 0; i < 4; i++) {
-        const int32_t b = cand[i];
-        if (b > y0 && b <= y1 && g_solid_class(T, h, b) != g_solid_class(T, h, b - 1)) return G_MIXED;
-    }
-    return c0;
+    return terrain_region_class(T.id_of, T.view, hmin, hmax, y0, y1, G_EMPTY, G_MIXED);
 }
 
 __global__ void k_heights(const uint8_t* perms, int32_t W, int32_t L, int16_t* h, int32_t* bad) {
@@ -222,7 +214,7 @@ int for_region_chunks(int64_t n, F&& launch) {
     return SVO_OK;
 }
 
-int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& pool, int32_t device, svo_tree** out) {
+int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& pool, int32_t device, int32_t view, svo_tree** out) {
     const int32_t E = 1 << (2 * levels);
     DevTerrain T;
     memset(&T, 0, sizeof(T));
@@ -232,7 +224,8 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
     T.L = L;
     T.h = dh;
     T.id_of[TM_AIR] = G_EMPTY;
-    T.id_of[TM_WATER] = G_EMPTY;
+    T.id_of[TM_WATER] = view ? 4u : G_EMPTY;
+    T.view = view;
     T.id_of[TM_GRASS] = 1;
     T.id_of[TM_DIRT] = 2;
     T.id_of[TM_STONE] = 3;
@@ -264,6 +257,7 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
     if (!t) SVO_FAIL(SVO_ENOMEM, "svo_build_terrain_gpu: out of memory");
     std::unique_ptr<svo_tree> guard(t);
     t->levels = levels;
+    t->view = view;
     t->palette.push_back(Material{0, ~0ull, 0.0f});
     t->palette.push_back(Material{1u, rgb_to_u64(0, 150, 10), 0.0f});         // 1 grass
     t->palette.push_back(Material{1u, rgb_to_u64(45, 18, 0), 0.0f});          // 2 dirt
@@ -387,7 +381,12 @@ int build_on_device(int32_t levels, int32_t W, int32_t L, int16_t* dh, Pool& poo
 }  // namespace
 
 extern "C" int svo_build_terrain_gpu(int32_t levels, int32_t width, int32_t length, int32_t device, svo_tree** out) {
+    return svo_build_terrain_gpu_view(levels, width, length, device, SVO_VIEW_SOLID, out);
+}
+
+extern "C" int svo_build_terrain_gpu_view(int32_t levels, int32_t width, int32_t length, int32_t device, int32_t view, svo_tree** out) {
     if (!out) SVO_FAIL(SVO_EINVAL, "svo_build_terrain_gpu: out is NULL");
+    if (view != SVO_VIEW_SOLID && view != SVO_VIEW_ALL) SVO_FAIL(SVO_EINVAL, "svo_build_terrain_gpu: unknown view");
     if (levels < 2 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_build_terrain_gpu: levels must be in [2, 7]");
     const int32_t E = 1 << (2 * levels);
     if (width < 1 || length < 1 || width > E || length > E) SVO_FAIL(SVO_EINVAL, "svo_build_terrain_gpu: columns must fit the extent");
@@ -420,7 +419,7 @@ extern "C" int svo_build_terrain_gpu(int32_t levels, int32_t width, int32_t leng
     int32_t bad = 0;
     HIP_TRY(hipMemcpy(&bad, dbad, 4, hipMemcpyDeviceToHost), SVO_EDEVICE);
     if (bad) SVO_FAIL(SVO_ERANGE, "svo_build_terrain_gpu: a column top falls outside [0, 32767]");
-    return build_on_device(levels, width, length, dh, pool, device, out);
+    return build_on_device(levels, width, length, dh, pool, device, view, out);
 }
 
 extern "C" int svo_build_heightfield_gpu(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t device,
@@ -443,5 +442,5 @@ extern "C" int svo_build_heightfield_gpu(int32_t levels, int32_t width, int32_t 
     int rc = pool.alloc(&dh, hg.size());
     if (rc) return rc;
     HIP_TRY(hipMemcpy(dh, hg.data(), hg.size() * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
-    return build_on_device(levels, width, length, dh, pool, device, out);
+    return build_on_device(levels, width, length, dh, pool, device, SVO_VIEW_SOLID, out);
 }

@@ -70,6 +70,9 @@ struct CastParams {
     float sun[3];
     int32_t look[3];
     int32_t look_valid, shadow_steps;
+    float time;                 // deltaTime of the liquid wobble (low_res.frag:226)
+    const Node* snodes;         // shading: the solid-view tree the shadow rays walk (nodes: the scene)
+    const uint16_t* smats;
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
@@ -476,8 +479,8 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
     return res;
 }
 
-__device__ __forceinline__ uint32_t brick_material(const CastParams& P, uint64_t mask, uint32_t ref, uint32_t info, uint32_t v) {
-    return (info & K_UNIFORM) ? (info >> 16) : (uint32_t)P.mats[ref + (uint32_t)__popcll(mask & ((1ull << v) - 1ull))];
+__device__ __forceinline__ uint32_t brick_material(const uint16_t* mats, uint64_t mask, uint32_t ref, uint32_t info, uint32_t v) {
+    return (info & K_UNIFORM) ? (info >> 16) : (uint32_t)mats[ref + (uint32_t)__popcll(mask & ((1ull << v) - 1ull))];
 }
 
 __device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) {
@@ -529,22 +532,20 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
 }
 
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
-// direction after them, reflection count, finalColorMod, and whether the ray was bent.
+// direction after them, reflection count, finalColorMod (a vec3: liquid tints per channel), and
+// whether the ray was bent.
 struct Bounce {
     float d[3];
     int32_t n;
-    float m;
+    float m[3];
     bool bent;
 };
 
-// refractRay(vec3, vec3, float, float) (low_res.frag:196-209), n1 = 1.0, n2 = 1.1, normal = the hit
-// axis times its step (:222-223); dot as ((x + y) + z), no fused operations (-ffp-contract=off)
-__device__ __forceinline__ void refract_dir(float d[3], uint32_t ax, int32_t st_ax) {
+// refractRay(vec3, vec3, float, float) (low_res.frag:196-209), n1 = 1.0, n2 = 1.1; dot as
+// ((x + y) + z), no fused operations (-ffp-contract=off)
+__device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
     const float r = 1.0f / 1.1f;
-    float n[3] = {0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int k = 0; k < 3; k++)
-        if (ax == (uint32_t)k) n[k] = (float)st_ax;
+    float n[3] = {nin[0], nin[1], nin[2]};
     float c1 = (n[0] * d[0] + n[1] * d[1]) + n[2] * d[2];
     if (c1 < 0.0f) {
 #pragma unroll
@@ -560,7 +561,7 @@ __device__ __forceinline__ void refract_dir(float d[3], uint32_t ax, int32_t st_
 // par_out: receives the parent of the region the ray ended in (it holds the final voxel; the LDS
 // path holds its ancestors at depths 0 .. levels-1-sh/2)
 template <bool STATS, bool REFLECT = false, class Mem>
-__device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const Path& path, const float o[3],
+__device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr) {
     Ray R;
@@ -650,7 +651,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             bool solid;
             v = brick_walk<STATS>(R, bmask, w, left0, left, solid, st);
             if (solid) {
-                mat = brick_material(P, bmask, bref, binfo, v);
+                mat = brick_material(mats, bmask, bref, binfo, v);
                 done = true;
             } else if (R.steps <= 0 && (((left - 0x010101u) & ~left & 0x808080u) == 0u)) {
                 done = true;  // budget ended inside the brick
@@ -660,7 +661,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             R.r[1] = step_by(R.r[1], (int32_t)((dn >> 8) & 0xFFu), R.s[1], REFLECT ? 0u : ud[1]);
             R.r[2] = step_by(R.r[2], (int32_t)(dn >> 16), R.s[2], REFLECT ? 0u : ud[2]);
         }
-        const uint32_t mflags = REFLECT && mat != kNoHit ? (P.mat_flags[mat] & 7u) : 0u;
+        const uint32_t mfl = REFLECT && mat != kNoHit ? P.mat_flags[mat] : 0u;
+        const uint32_t mflags = mfl & 7u;
         if (REFLECT && R.steps > 0 && mflags == 3u) {
             // a reflective block (flags & 7 == 3) with budget left: undo the last crossing on the
             // hit axis, mirror that axis (step and direction) and take the next DDA step from the
@@ -675,36 +677,48 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 }
             }
             bounce->n++;
-            bounce->m *= 0.94f;
+#pragma unroll
+            for (int k = 0; k < 3; k++) bounce->m[k] *= 0.94f;
             dda_step(R);
             done = false;
             mat = kNoHit;
         } else if (REFLECT && R.steps > 0 && mflags == 5u) {
-            // a refractive solid (liquid is empty here, as in castRayFromCam) with budget left:
-            // tint by 0.95 and pass; the first one bends the ray (refractRay, :211-240).  The
-            // shader's exact position is never advanced by its DDA: it is the origin (minus 1 on
-            // axes with a negative initial step), +1 on the other axes with a negative step, then
-            // min(new step, 0); deltaPos restarts from the current cell.
-            bounce->m *= 0.95f;
+            // a refractive block (glass, or liquid when the scene tree holds it) with budget left:
+            // tint (liquid (0.94, 0.97, 1.0), else 0.95) and pass; the first one bends the ray
+            // (refractRay, :211-240).  The shader's exact position is never advanced by its DDA: it
+            // is the origin (minus 1 on axes with a negative initial step), +1 on the other axes with
+            // a negative step, then min(new step, 0); deltaPos restarts from the current cell.
+            const bool liquid = (mfl & 0x10u) != 0u;
+            bounce->m[0] *= liquid ? 0.94f : 0.95f;
+            bounce->m[1] *= liquid ? 0.97f : 0.95f;
+            bounce->m[2] *= liquid ? 1.0f : 0.95f;
             if (!bounce->bent) {
                 bounce->bent = true;
                 const uint32_t ax = R.axis;
-                int32_t sa = 1;
-#pragma unroll
-                for (int k = 0; k < 3; k++)
-                    if (ax == (uint32_t)k) sa = R.s[k];
-                refract_dir(bounce->d, ax, sa);
+                double ex[3];
+                float nrm[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
-                    double ex = (double)o[k];
-                    if (d[k] < 0.0f) ex -= 1.0;
-                    if (ax != (uint32_t)k && R.s[k] < 0) ex += 1.0;
+                    ex[k] = (double)o[k];
+                    if (d[k] < 0.0f) ex[k] -= 1.0;
+                    if (ax != (uint32_t)k && R.s[k] < 0) ex[k] += 1.0;
+                    if (ax == (uint32_t)k) nrm[k] = (float)R.s[k];
+                }
+                if (liquid) {
+                    // the wave wobble (:225-229) at the shader's (float) exact position
+                    const float arg = ((P.time + (float)ex[0] * 0.2f) - (float)ex[2] * 0.1f) * 10.0f;
+                    nrm[0] += svo::sin_f32(arg) * 0.2f;
+                    normalize3(nrm, nrm);
+                }
+                refract_dir(bounce->d, nrm);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
                     const float dk = bounce->d[k];
                     const int32_t s = dk < 0.0f ? -1 : 1;
                     const double delta = (double)svo::div_rn(1.0f, dk);
                     const double ad = delta >= 0.0 ? delta : -delta;
-                    if (s < 0) ex -= 1.0;
-                    R.T[k] = ad - (ex - (double)R.r[k]) * delta;
+                    if (s < 0) ex[k] -= 1.0;
+                    R.T[k] = ad - (ex[k] - (double)R.r[k]) * delta;
                     R.s[k] = s;
                     R.af[k] = (float)ad;
                     R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
@@ -882,6 +896,7 @@ template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE>
 __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
+    const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
     if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
@@ -958,22 +973,22 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         out = 0;
     }
     if (SHADE && out >= 0) {
-        Bounce bn = {{d[0], d[1], d[2]}, 0, 1.0f, false};
-        const Hit h = trace<false, true>(P, mem, path, o, d, P.steps, nullptr, &bn);
+        Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
+        const Hit h = trace<false, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
             P.info[out] = h.info;
         }
         const bool hit = (h.info & HIT_BIT) != 0u;
-        const float m = bn.m;  // finalColorMod
+        const float* m = bn.m;  // finalColorMod
         float3 c;
         if (P.look_valid && h.x == P.look[0] && h.y == P.look[1] && h.z == P.look[2]) {
             const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
             c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
         } else if (!hit) {
             const float3 sk = sky_color(bn.d, P.sun);
-            c = make_float3(sk.x * m, sk.y * m, sk.z * m);
+            c = make_float3(sk.x * m[0], sk.y * m[1], sk.z * m[2]);
         } else {
             const float3 col = color_of(P.mat_color[h.info & MAT_MASK]);
             const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
@@ -981,7 +996,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
             const float l = (ax == 0u ? P.sun[0] : (ax == 1u ? P.sun[1] : P.sun[2])) * (float)(-sg);
             const bool facing = l > 0.0f;
             const float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
-            c = make_float3(col.x * inten * m, col.y * inten * m, col.z * inten * m);
+            c = make_float3(col.x * inten * m[0], col.y * inten * m[1], col.z * inten * m[2]);
             bool dark = false;
             if (bn.n == 0) {
                 if (!facing) {
@@ -990,15 +1005,15 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                     // shadow ray towards the sun from the centre of lastPos, through empty and liquid
                     const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                          (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                    dark = (trace<false>(P, mem, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
+                    dark = (trace<false>(P, smem, P.smats, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
                 }
             }
-            if (dark) c = make_float3(col.x * 0.3f * m, col.y * 0.3f * m, col.z * 0.3f * m);
+            if (dark) c = make_float3(col.x * 0.3f * m[0], col.y * 0.3f * m[1], col.z * 0.3f * m[2]);
         }
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS>(P, mem, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
@@ -1019,7 +1034,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                     const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
                     float ad[3];
                     ao_dir(hv, ax, -st, ad);
-                    const Hit a = trace<false>(P, mem, path, ao_o, ad, P.ao_steps);
+                    const Hit a = trace<false>(P, mem, P.mats, path, ao_o, ad, P.ao_steps);
                     cnt += (a.info & HIT_BIT) ? 1u : 0u;
                 }
                 }
@@ -1360,6 +1375,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
                               const svo_hits* o, void* stream) {
     if (!t || !d || !sd || !rgba) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: NULL argument");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_shade_rays: tree not uploaded (svo_upload)");
+    if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: t must be a solid-view tree (the scene goes in svo_shade_desc.scene)");
     if (d->steps < 0 || sd->shadow_steps < 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: negative step budget");
     if (d->ao_samples != 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: AO is a separate pass (ao_samples must be 0)");
     if (d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: no diagnostics in the shading pass");
@@ -1369,11 +1385,17 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     } else if (d->width <= 0 || d->height <= 0 || d->tile_row_step <= 0 || d->tile_row_start < 0) {
         SVO_FAIL(SVO_EINVAL, "svo_shade_rays: bad frame geometry");
     }
+    const svo_tree* sc = sd->scene ? sd->scene : t;
+    if (sc->device != t->device) SVO_FAIL(SVO_ESTATE, "svo_shade_rays: scene tree not uploaded to the tree's device");
+    if (sc->levels != t->levels) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: scene and tree differ in levels");
     const svo_hits none = {nullptr, nullptr, nullptr, nullptr};
     CastParams P;
     int64_t n = 0;
-    int rc = fill_params(t, d, o ? o : &none, P, n);
+    int rc = fill_params(sc, d, o ? o : &none, P, n);
     if (rc) return rc;
+    P.snodes = reinterpret_cast<const Node*>(t->d_nodes);
+    P.smats = reinterpret_cast<const uint16_t*>(t->d_mats);
+    P.time = sd->time;
     P.rgba = reinterpret_cast<float4*>(rgba);
     for (int k = 0; k < 3; k++) {
         P.sun[k] = sd->sun_dir[k];
@@ -1385,7 +1407,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
-    launch_cast<false, false, false, true>(wide_nodes(t, d->flags), dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
+    launch_cast<false, false, false, true>(wide_nodes(t, d->flags) || wide_nodes(sc, d->flags), dim3((uint32_t)blocks), dim3(kBlock),
+                                           (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -1394,6 +1417,7 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (!t || !d || !o) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL argument");
     if (!o->pos_steps || !o->t || !o->info) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL output buffer");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_rays: tree not uploaded (svo_upload)");
+    if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: castRayFromCam semantics need a solid-view tree");
     if (d->steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative step budget");
     if ((d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) && !d->stats)
         SVO_FAIL(SVO_EINVAL, "svo_cast_rays: SVO_CAST_STATS / TIMELINE without a stats buffer");
@@ -1433,6 +1457,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
                                      svo_block* block) {
     if (!t || !pos || !dir || !out) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: NULL argument");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_ray_from_cam: tree not uploaded (svo_upload)");
+    if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: castRayFromCam semantics need a solid-view tree");
     if (steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: negative step budget");
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     void* buf = nullptr;

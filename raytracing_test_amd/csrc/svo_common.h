@@ -76,6 +76,25 @@ SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
 SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
 #endif
 
+// sin of a float through double precision, rounded once to float (the shading pass's liquid wobble,
+// low_res.frag:226): Cody-Waite reduction by pi/2 (k * PIO2_HI is exact for |k| < 2^20), Taylor
+// polynomials of sin / cos on [-pi/4, pi/4] (truncation < 3e-14), the quadrant's sign and function.
+// The same double operations on host and device (no contraction), so both round alike; far cheaper
+// in registers than a libm sin.
+SVO_HD float sin_f32(float xf) {
+    const double x = (double)xf;
+    const double k = __builtin_rint(x * 0.63661977236758134308);
+    const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
+    const double r2 = r * r;
+    const double sn = r + (r * r2) * (-1.6666666666666666e-01 + r2 * (8.3333333333333332e-03 + r2 * (-1.9841269841269841e-04 +
+                                     r2 * (2.7557319223985893e-06 + r2 * (-2.5052108385441720e-08 + r2 * 1.6059043836821613e-10)))));
+    const double cs = 1.0 + r2 * (-0.5 + r2 * (4.1666666666666664e-02 + r2 * (-1.3888888888888889e-03 + r2 * (2.4801587301587302e-05 +
+                                  r2 * (-2.7557319223985888e-07 + r2 * (2.0876756987868100e-09 + r2 * -1.1470745597729725e-11))))));
+    const int64_t q = (int64_t)k & 3;
+    const double v = (q & 1) ? cs : sn;
+    return (float)((q & 2) ? -v : v);
+}
+
 // glm::cross (x.y*y.z - y.y*x.z, x.z*y.x - y.z*x.x, x.x*y.y - y.x*x.y)
 SVO_HD void cross3(const float a[3], const float b[3], float o[3]) {
     o[0] = a[1] * b[2] - b[1] * a[2];

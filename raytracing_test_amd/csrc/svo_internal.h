@@ -22,6 +22,9 @@ inline bool material_solid(const Material& m) {
     return m.color != ~0ull && (m.flags & 0x10u) == 0;
 }
 
+// stored by a tree of `view` (SVO_VIEW_SOLID: what castRayFromCam hits; SVO_VIEW_ALL: every block)
+inline bool material_in_view(const Material& m, int32_t view) { return view ? m.color != ~0ull : material_solid(m); }
+
 void set_error(const std::string& msg);
 
 // RGB_TO_U64 (src/types.hpp:6-9)
@@ -37,6 +40,7 @@ inline uint64_t rgb_to_u64(int r, int g, int b) {
 // Linearised tree: host image + optional HBM copy
 struct svo_tree {
     int32_t levels = 0;
+    int32_t view = 0;                     // SVO_VIEW_SOLID / SVO_VIEW_ALL
     std::vector<svo::Node> nodes;
     std::vector<uint16_t> mats;           // per-voxel material ids of mixed-material bricks
     std::vector<svo::Material> palette;   // id 0 = empty block {0, ~0, 0}

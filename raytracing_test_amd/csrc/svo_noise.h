@@ -118,4 +118,31 @@ SVO_HD uint32_t terrain_material(int32_t h, int32_t y) {
     return y >= h - 3 ? TM_DIRT : TM_STONE;
 }
 
+// Tree views (include/svo_rt.h SVO_VIEW_*): the solid view stores what castRayFromCam hits (water is
+// empty, ray_caster.cpp:82); the full view stores every block genWorld puts, water included.
+// Stored top of a column: its top voxel, or the water surface (y = 20) over a top below 20.
+SVO_HD int32_t terrain_top(int32_t h, int32_t view) { return (view && h < 20) ? 20 : h; }
+
+// Class of an aligned region of rows y0..y1 over a full footprint of columns whose tops span
+// [hmin, hmax]: `empty`, a uniform material id_of[terrain material], or `mixed`.  Emptiness comes
+// first (callers treat a non-empty region over a partial footprint as mixed).
+SVO_HD bool terrain_region_empty(int32_t view, int32_t hmax, int32_t y0, int32_t y1) {
+    return y1 < 1 || y0 > terrain_top(hmax, view);
+}
+SVO_HD uint32_t terrain_region_class(const uint32_t id_of[5], int32_t view, int32_t hmin, int32_t hmax, int32_t y0, int32_t y1,
+                                     uint32_t empty, uint32_t mixed) {
+    if (terrain_region_empty(view, hmax, y0, y1)) return empty;
+    if (y0 >= 1 && y1 <= hmin - 4) return id_of[TM_STONE];
+    if (view && y0 > hmax && y1 <= 20) return id_of[TM_WATER];  // above every top, below the surface
+    if (hmin != hmax) return mixed;  // dirt / grass runs are < 4 voxels unless all columns agree
+    const int32_t h = hmin;
+    const uint32_t c0 = id_of[terrain_material(h, y0)];
+    const int32_t cand[5] = {1, h - 3, h, h + 1, 21};  // where a column's material can change
+    for (int i = 0; i < 5; i++) {
+        const int32_t b = cand[i];
+        if (b > y0 && b <= y1 && id_of[terrain_material(h, b)] != id_of[terrain_material(h, b - 1)]) return mixed;
+    }
+    return c0;
+}
+
 }  // namespace svo

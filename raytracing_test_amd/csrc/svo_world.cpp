@@ -387,11 +387,14 @@ static void finish_tree_stats(svo_tree* t) {
     (void)t;
 }
 
-extern "C" int svo_build(const svo_world* w, svo_tree** out) {
+extern "C" int svo_build(const svo_world* w, svo_tree** out) { return svo_build_view(w, SVO_VIEW_SOLID, out); }
+
+extern "C" int svo_build_view(const svo_world* w, int32_t view, svo_tree** out) {
     if (!w || !out) SVO_FAIL(SVO_EINVAL, "svo_build: NULL argument");
+    if (view != SVO_VIEW_SOLID && view != SVO_VIEW_ALL) SVO_FAIL(SVO_EINVAL, "svo_build_view: unknown view");
     const int L = w->levels;
     std::vector<uint8_t> solid(w->pal.m.size());
-    for (size_t i = 0; i < solid.size(); i++) solid[i] = material_solid(w->pal.m[i]);
+    for (size_t i = 0; i < solid.size(); i++) solid[i] = material_in_view(w->pal.m[i], view);
     // post-order classes of every live edit node
     std::vector<uint32_t> cls(w->nodes.size(), C_EMPTY);
     std::function<uint32_t(uint32_t, int)> classify = [&](uint32_t n, int depth) -> uint32_t {
@@ -413,6 +416,7 @@ extern "C" int svo_build(const svo_world* w, svo_tree** out) {
     svo_tree* t = new (std::nothrow) svo_tree();
     if (!t) SVO_FAIL(SVO_ENOMEM, "svo_build: out of memory");
     t->levels = L;
+    t->view = view;
     t->palette = w->pal.m;
     // level-synchronous emission; `cur` = edit ids of this depth's nodes (in node order)
     std::vector<uint32_t> cur{0};
@@ -578,7 +582,7 @@ extern "C" int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* x
         t->palette_dirty = true;
     }
     Emitter em{t, w, std::vector<uint8_t>(w->pal.m.size()), {}};
-    for (size_t i = 0; i < em.solid.size(); i++) em.solid[i] = material_solid(w->pal.m[i]);
+    for (size_t i = 0; i < em.solid.size(); i++) em.solid[i] = material_in_view(w->pal.m[i], t->view);
     const uint32_t mk = (1u << (2 * L)) - 1u;
     bool rebuild = de == 0 || node_kind(t->nodes[0].info) != K_INTERIOR;
     for (int64_t i = 0; i < n && !rebuild; i++) {
@@ -625,7 +629,7 @@ extern "C" int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* x
     }
     if (rebuild || t->garbage_nodes * 2 > t->nodes.size()) {
         svo_tree* f = nullptr;
-        int rc = svo_build(w, &f);
+        int rc = svo_build_view(w, t->view, &f);
         if (rc) return rc;
         t->nodes.swap(f->nodes);
         t->mats.swap(f->mats);
@@ -657,14 +661,16 @@ struct TerrainCtx {
     int32_t levels, E, W, L;
     const int16_t* h;  // [x*L + z]
     Pyramid pyr;
-    uint32_t id_of[5];  // terrain material -> palette id (0 for non-solid)
+    uint32_t id_of[5];  // terrain material -> palette id (0 for non-stored)
+    int32_t view;       // SVO_VIEW_SOLID / SVO_VIEW_ALL
 };
 
 inline uint32_t solid_class(const TerrainCtx& T, int32_t h, int32_t y) {
     return T.id_of[terrain_material(h, y)];
 }
 
-// class of the aligned region [x0,x0+s) x [y0,y0+s) x [z0,z0+s), s = 4^k >= 4
+// class of the aligned region [x0,x0+s) x [y0,y0+s) x [z0,z0+s), s = 4^k >= 4 (svo_noise.h
+// terrain_region_class over the pyramid's min / max tops of its footprint)
 uint32_t classify_region(const TerrainCtx& T, int32_t x0, int32_t y0, int32_t z0, int32_t s, int k) {
     const int32_t y1 = y0 + s - 1;
     if (x0 >= T.W || z0 >= T.L) return C_EMPTY;  // no columns here
@@ -672,18 +678,9 @@ uint32_t classify_region(const TerrainCtx& T, int32_t x0, int32_t y0, int32_t z0
     const int32_t cx = x0 >> (2 * k), cz = z0 >> (2 * k);
     const size_t ci = (size_t)cx * T.pyr.dimz[k] + cz;
     const int32_t hmin = T.pyr.hmin[k][ci], hmax = T.pyr.hmax[k][ci];
-    if (y1 < 1 || y0 > hmax) return C_EMPTY;
+    if (terrain_region_empty(T.view, hmax, y0, y1)) return C_EMPTY;
     if (partial) return C_MIXED;
-    if (y0 >= 1 && y1 <= hmin - 4) return T.id_of[TM_STONE];
-    if (hmin != hmax) return C_MIXED;  // dirt / grass runs are < 4 voxels unless all columns agree
-    const int32_t h = hmin;
-    const uint32_t c0 = solid_class(T, h, y0);
-    const int32_t cand[4] = {1, h - 3, h, h + 1};
-    for (int i = 0; i < 4; i++) {
-        const int32_t b = cand[i];
-        if (b > y0 && b <= y1 && solid_class(T, h, b) != solid_class(T, h, b - 1)) return C_MIXED;
-    }
-    return c0;
+    return terrain_region_class(T.id_of, T.view, hmin, hmax, y0, y1, C_EMPTY, C_MIXED);
 }
 
 void brick_voxels(const TerrainCtx& T, int32_t x0, int32_t y0, int32_t z0, uint32_t vox[64]) {
@@ -701,11 +698,16 @@ struct Region {
 };
 }  // namespace
 
-static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, std::vector<int16_t>& hg,
+static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, int32_t view, std::vector<int16_t>& hg,
                               svo_tree** out);
 
 extern "C" int svo_build_terrain(int32_t levels, int32_t width, int32_t length, int32_t nthreads, svo_tree** out) {
+    return svo_build_terrain_view(levels, width, length, nthreads, SVO_VIEW_SOLID, out);
+}
+
+extern "C" int svo_build_terrain_view(int32_t levels, int32_t width, int32_t length, int32_t nthreads, int32_t view, svo_tree** out) {
     if (!out) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: out is NULL");
+    if (view != SVO_VIEW_SOLID && view != SVO_VIEW_ALL) SVO_FAIL(SVO_EINVAL, "svo_build_terrain_view: unknown view");
     if (levels < 2 || levels > 7) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: levels must be in [2, 7]");
     const int32_t E = 1 << (2 * levels);
     if (width < 1 || length < 1 || width > E || length > E) SVO_FAIL(SVO_EINVAL, "svo_build_terrain: columns must fit the extent");
@@ -725,7 +727,7 @@ extern "C" int svo_build_terrain(int32_t levels, int32_t width, int32_t length, 
             }
     });
     if (bad) SVO_FAIL(SVO_ERANGE, "svo_build_terrain: a column top falls outside [0, 32767]");
-    return build_from_heights(levels, width, length, nthreads, hg, out);
+    return build_from_heights(levels, width, length, nthreads, view, hg, out);
 }
 
 extern "C" int svo_build_heightfield(int32_t levels, int32_t width, int32_t length, const int32_t* heights, int32_t nthreads,
@@ -739,10 +741,10 @@ extern "C" int svo_build_heightfield(int32_t levels, int32_t width, int32_t leng
         if (heights[i] < 0 || heights[i] > 32767) SVO_FAIL(SVO_ERANGE, "svo_build_heightfield: heights must be in [0, extent-2]");
         hg[i] = (int16_t)heights[i];
     }
-    return build_from_heights(levels, width, length, nthreads, hg, out);
+    return build_from_heights(levels, width, length, nthreads, SVO_VIEW_SOLID, hg, out);
 }
 
-static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, std::vector<int16_t>& hg,
+static int build_from_heights(int32_t levels, int32_t width, int32_t length, int32_t nthreads, int32_t view, std::vector<int16_t>& hg,
                               svo_tree** out) {
     const int32_t E = 1 << (2 * levels);
     for (size_t i = 0; i < hg.size(); i++)
@@ -754,6 +756,7 @@ static int build_from_heights(int32_t levels, int32_t width, int32_t length, int
     T.W = width;
     T.L = length;
     T.h = hg.data();
+    T.view = view;
     // ---- min/max pyramid over aligned 4^k footprints
     T.pyr.W = width;
     T.pyr.L = length;
@@ -790,6 +793,7 @@ static int build_from_heights(int32_t levels, int32_t width, int32_t length, int
     svo_tree* t = new (std::nothrow) svo_tree();
     if (!t) SVO_FAIL(SVO_ENOMEM, "svo_build_terrain: out of memory");
     t->levels = levels;
+    t->view = view;
     // palette: the blocks genWorld stores (stored flags = 1 | Block.flags)
     t->palette.push_back(Material{0, ~0ull, 0.0f});
     t->palette.push_back(Material{1u, rgb_to_u64(0, 150, 10), 0.0f});  // 1 grass
@@ -797,7 +801,7 @@ static int build_from_heights(int32_t levels, int32_t width, int32_t length, int
     t->palette.push_back(Material{1u, rgb_to_u64(33, 33, 33), 0.0f});  // 3 stone
     t->palette.push_back(Material{1u | 0x14u, rgb_to_u64(0, 150, 10), 0.0f});  // 4 water (LIQUID)
     T.id_of[TM_AIR] = C_EMPTY;
-    T.id_of[TM_WATER] = C_EMPTY;
+    T.id_of[TM_WATER] = view ? 4u : C_EMPTY;
     T.id_of[TM_GRASS] = 1;
     T.id_of[TM_DIRT] = 2;
     T.id_of[TM_STONE] = 3;
@@ -930,6 +934,7 @@ extern "C" int svo_tree_get_info(const svo_tree* t, svo_tree_info* o) {
     for (int i = 0; i < 8; i++) o->nodes_per_level[i] = t->nodes_per_level[i];
     o->device_bytes = t->device_bytes;
     o->device = t->device;
+    o->view = t->view;
     return SVO_OK;
 }
 

@@ -17,7 +17,7 @@ def _probe_points(rng, edits, extent, n_random=20000):
 
 
 def _same_as_fresh(rt, world, tree, pts):
-    fresh = world.build()
+    fresh = world.build(tree.info().view)
     got, want = tree.get_blocks(pts), fresh.get_blocks(pts)
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, "%d positions differ, first %s: patched %s fresh %s" % (len(bad), pts[bad[:3]], got[bad[:3]], want[bad[:3]])
@@ -27,10 +27,12 @@ def _random_edits(rng, n, lo, hi):
     return np.stack([rng.integers(lo[0], hi[0], n), rng.integers(lo[1], hi[1], n), rng.integers(lo[2], hi[2], n)], 1)
 
 
-def test_voxel_edits_match_rebuild(rt):
+@pytest.mark.parametrize("view", [0, 1])
+def test_voxel_edits_match_rebuild(rt, view):
+    """edits keep the tree's view (SVO_VIEW_ALL: liquid puts are stored too)"""
     rng = np.random.default_rng(7)
     w = rt.World.reference()
-    tree = w.build()
+    tree = w.build(view)
     extent = 1 << (2 * w.levels)
     n0 = tree.info().n_nodes
     all_edits = []

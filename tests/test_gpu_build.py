@@ -27,9 +27,12 @@ def _same(a, b, label):
     assert list(ia.nodes_per_level) == list(ib.nodes_per_level) and ia.n_bricks == ib.n_bricks, label
 
 
+@pytest.mark.parametrize("view", [0, 1])
 @pytest.mark.parametrize("levels,W,L", [(3, 64, 64), (4, 200, 200), (5, 1000, 700), (6, 1024, 1024)])
-def test_terrain_gpu_equals_host(rt, torch_cuda, levels, W, L):
-    _same(rt.Tree.terrain_gpu(levels, W, L, 0), rt.Tree.terrain(levels, W, L), "terrain L%d %dx%d" % (levels, W, L))
+def test_terrain_gpu_equals_host(rt, torch_cuda, levels, W, L, view):
+    g, h = rt.Tree.terrain_gpu(levels, W, L, 0, view=view), rt.Tree.terrain(levels, W, L, view=view)
+    assert g.info().view == view
+    _same(g, h, "terrain L%d %dx%d view %d" % (levels, W, L, view))
 
 
 def test_heightfield_gpu_equals_host(rt, torch_cuda):

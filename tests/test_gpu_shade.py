@@ -157,3 +157,62 @@ def test_shade_refraction(rt, glass_worlds, cam):
         plain = rt.decode_hits(gt.cast_frame(org, cam_dir, 240, 136, S))["pos"]
         moved = np.any(rt.decode_hits(hits)["pos"] != plain, axis=1).sum()
         assert moved > 500, moved
+
+
+# ---- liquid (low_res.frag:214-229, :325-326): water refracts and tints when the scene holds it --
+LAKE_CAMERAS = [
+    ((4.0, 90.0, 4.0), (1.0, -0.45, 1.0)),        # C1 pose: the lakes around (150, 20, 158) far ahead
+    ((150.5, 40.25, 120.5), (0.1, -0.6, 1.0)),    # looking down into a lake
+    ((151.5, 15.5, 157.5), (0.7, 0.2, -0.4)),     # under water
+]
+
+
+@pytest.fixture(scope="module")
+def lake_scene(rt, ref_world, torch_cuda):
+    return ref_world.build(rt.VIEW_ALL).upload(0)
+
+
+@pytest.mark.parametrize("cam", range(len(LAKE_CAMERAS)))
+@pytest.mark.parametrize("tm", [0.0, 2.75])
+def test_shade_liquid_reference_world(rt, gtree, lake_scene, ref_world_oracle, cam, tm):
+    """with the SVO_VIEW_ALL scene, water (flags 0x15) tints by (0.94, 0.97, 1.0) per voxel and the
+    first refractive voxel bends the ray with the wave wobble of time `tm`; against the oracle's
+    liquid mode, the same contract as the glass tests"""
+    org, cd = LAKE_CAMERAS[cam]
+    cam_dir = rt.normalize(cd)
+    W, H, S = 240, 136, 300
+    rgba, hits = gtree.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), with_hits=True, scene=lake_scene, time=tm)
+    ref = ref_world_oracle.shade_frame(org, cam_dir, W, H, S, rt.sun_dir(), liquid=True, time=tm)
+    _check(rgba, ref, rt.decode_hits(hits)["hit"], "lake cam%d t=%g" % (cam, tm))
+    # liquid is exercised: against the shading pass without the scene (water passes unbent)
+    dry = gtree.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir()).cpu().numpy()
+    assert np.any(dry != rgba.cpu().numpy(), axis=1).sum() > 300
+
+
+def test_shade_liquid_time_moves_the_bend(rt, gtree, lake_scene):
+    org, cd = LAKE_CAMERAS[1]
+    cam_dir = rt.normalize(cd)
+    a = rt.decode_hits(gtree.shade_frame(org, cam_dir, 160, 90, 300, sun=rt.sun_dir(), with_hits=True, scene=lake_scene, time=0.0)[1])
+    b = rt.decode_hits(gtree.shade_frame(org, cam_dir, 160, 90, 300, sun=rt.sun_dir(), with_hits=True, scene=lake_scene, time=0.37)[1])
+    assert np.any(a["pos"] != b["pos"], axis=1).sum() > 100
+
+
+def test_shade_liquid_depth12_sampled(rt, oracle_mod, torch_cuda):
+    """C3 pose over 1024^2 terrain columns with their lakes: the GPU-built full-view scene, sampled
+    pixels against the oracle's terrain tree in liquid mode"""
+    W, H = 1920, 1080
+    tree = rt.Tree.terrain_gpu(6, 1024, 1024, 0)
+    scene = rt.Tree.terrain_gpu(6, 1024, 1024, 0, view=rt.VIEW_ALL)
+    org, cam_dir = (4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0))
+    rgba, hits = tree.shade_frame(org, cam_dir, W, H, 16384, sun=rt.sun_dir(), with_hits=True, scene=scene, time=1.25)
+    ot = oracle_mod.Tree.terrain(6, 1024, 1024)
+    pix = np.random.default_rng(6).choice(W * H, 4000, replace=False)
+    ref = ot.shade_frame(org, cam_dir, W, H, 16384, rt.sun_dir(), pixels=pix, liquid=True, time=1.25)
+    g = rt.decode_hits(hits)
+    _check(rgba[torch_cuda.as_tensor(pix, device=rgba.device)], ref, g["hit"][pix], "depth12 lakes")
+
+
+def test_full_view_tree_is_not_castable(rt, lake_scene):
+    """castRayFromCam semantics need the solid view: a full-view tree is refused, not silently cast"""
+    with pytest.raises(RuntimeError):
+        lake_scene.cast_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 16, 16, 300)

@@ -20,7 +20,7 @@ def test_abi_exports_every_declared_symbol(rt):
     L = C.CDLL(rt.LIB_PATH)
     for s in declared:
         assert hasattr(L, s), s
-    assert rt.lib().svo_version() == 3
+    assert rt.lib().svo_version() == 4
 
 
 def test_product_noise_matches_reference_golden(rt):
@@ -61,16 +61,42 @@ def test_linearised_tree_matches_solid_view(rt, ref_tree, ref_world_oracle):
     assert np.all(ids[~solid] == 0)
 
 
-def test_terrain_builder_equals_edit_builder(rt):
+@pytest.mark.parametrize("view", [0, 1])
+def test_terrain_builder_equals_edit_builder(rt, view):
+    """the column builder (min/max pyramid classes, svo_noise.h terrain_region_class) emits what the
+    edit-tree builder emits from genWorld's putBlocks, in both views (SVO_VIEW_ALL stores the water)"""
     for levels, W, L in ((4, 256, 256), (4, 200, 150), (5, 300, 1024)):
         w = rt.World(levels)
         w.gen_world(W, L)
-        a = w.build()
-        b = rt.Tree.terrain(levels, W, L)
+        a = w.build(view)
+        b = rt.Tree.terrain(levels, W, L, view=view)
+        assert a.info().view == b.info().view == view
         na, ma = a.export()
         nb, mb = b.export()
         assert a.palette() == b.palette()
         assert np.array_equal(na, nb) and np.array_equal(ma, mb), (levels, W, L)
+
+
+def test_full_view_stores_liquid(rt, ref_world):
+    """SVO_VIEW_ALL (the shading scene) holds every stored block, water included; the solid view
+    (castRayFromCam, ray_caster.cpp:82) leaves liquid empty; both agree everywhere else"""
+    a, b = ref_world.build(), ref_world.build(rt.VIEW_ALL)
+    g = np.stack(np.meshgrid(np.arange(0, 210, 3), np.arange(0, 40), np.arange(0, 210, 3), indexing="ij"), -1).reshape(-1, 3)
+    f, c, _ = ref_world.get_blocks(g)
+    ida, idb = a.get_blocks(g), b.get_blocks(g)
+    liq = (f & rt.LIQUID) != 0
+    assert liq.sum() > 1000  # the reference world's lakes
+    assert np.all(ida[liq] == 0) and np.all(idb[liq] != 0)
+    assert np.array_equal(ida[~liq], idb[~liq])
+    pal = b.palette()
+    assert all(pal[i][0] == 0x15 for i in np.unique(idb[liq]))  # REFRACTIVE | LIQUID | stored
+
+
+def test_oracle_sin_is_correctly_rounded(oracle_mod):
+    """the liquid wobble's sin (svo_common.h sin_f32 and its oracle restatement): float(sin(double))"""
+    xs = np.concatenate([np.linspace(-300, 300, 60001), np.random.default_rng(3).uniform(-9000, 9000, 20000)]).astype(np.float32)
+    got = np.array([oracle_mod.sin_f32(float(x)) for x in xs], np.float32)
+    assert np.array_equal(got, np.sin(xs.astype(np.float64)).astype(np.float32))
 
 
 def test_raygen_bit_exact_with_oracle(rt, oracle_mod):
