@@ -689,9 +689,12 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // is the origin (minus 1 on axes with a negative initial step), +1 on the other axes with
             // a negative step, then min(new step, 0); deltaPos restarts from the current cell.
             const bool liquid = (mfl & 0x10u) != 0u;
-            bounce->m[0] *= liquid ? 0.94f : 0.95f;
-            bounce->m[1] *= liquid ? 0.97f : 0.95f;
-            bounce->m[2] *= liquid ? 1.0f : 0.95f;
+            const float t0 = liquid ? 0.94f : 0.95f, t1 = liquid ? 0.97f : 0.95f, t2 = liquid ? 1.0f : 0.95f;
+            bounce->m[0] *= t0;
+            bounce->m[1] *= t1;
+            bounce->m[2] *= t2;
+            uint32_t wr[3];
+            wrap3(R, wm, wr);  // the refractive voxel (its region, when uniform, is passed below)
             if (!bounce->bent) {
                 bounce->bent = true;
                 const uint32_t ax = R.axis;
@@ -728,7 +731,27 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             }
             dda_step(R);
             done = false;
+            const uint32_t keep = mat;
             mat = kNoHit;
+            if (kind == R_SOLID) {
+                // the rest of a uniform refractive region (a lake's body): the same block voxel after
+                // voxel — tint and step without lookups; its 2^sh-wide aligned region is the child
+                // slot of `par` the lookup ended in.  A voxel reached with no budget left is the hit.
+                for (;;) {
+                    uint32_t w[3];
+                    wrap3(R, wm, w);
+                    if (((w[0] ^ wr[0]) | (w[1] ^ wr[1]) | (w[2] ^ wr[2])) >> par.sh) break;
+                    if (R.steps <= 0) {
+                        mat = keep;
+                        done = true;
+                        break;
+                    }
+                    bounce->m[0] *= t0;
+                    bounce->m[1] *= t1;
+                    bounce->m[2] *= t2;
+                    dda_step(R);
+                }
+            }
         }
     }
     const bool hit = mat != kNoHit;

@@ -163,7 +163,7 @@ def test_shade_refraction(rt, glass_worlds, cam):
 LAKE_CAMERAS = [
     ((4.0, 90.0, 4.0), (1.0, -0.45, 1.0)),        # C1 pose: the lakes around (150, 20, 158) far ahead
     ((150.5, 40.25, 120.5), (0.1, -0.6, 1.0)),    # looking down into a lake
-    ((151.5, 15.5, 157.5), (0.7, 0.2, -0.4)),     # under water
+    ((162.5, 16.5, 128.5), (0.7, 0.15, -0.4)),    # under water (column top 10)
 ]
 
 
@@ -186,7 +186,7 @@ def test_shade_liquid_reference_world(rt, gtree, lake_scene, ref_world_oracle, c
     _check(rgba, ref, rt.decode_hits(hits)["hit"], "lake cam%d t=%g" % (cam, tm))
     # liquid is exercised: against the shading pass without the scene (water passes unbent)
     dry = gtree.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir()).cpu().numpy()
-    assert np.any(dry != rgba.cpu().numpy(), axis=1).sum() > 300
+    assert np.any(dry != rgba.cpu().numpy(), axis=1).sum() > 100
 
 
 def test_shade_liquid_time_moves_the_bend(rt, gtree, lake_scene):
