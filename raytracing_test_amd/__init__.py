@@ -108,6 +108,8 @@ class CastDesc(C.Structure):
         ("stats", C.c_void_p),
         ("n_frames", C.c_int32),
         ("frame_origins", C.c_void_p),
+        ("wave_order", C.c_void_p),
+        ("wave_cost", C.c_void_p),
     ]
 
 
@@ -138,6 +140,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
+    "svo_cast_order",
 )
 
 
@@ -184,6 +187,7 @@ def lib():
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
     L.svo_cast_blocks.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
+    L.svo_cast_order.argtypes = [C.POINTER(CastDesc), vp, i32, vp, vp]
     L.svo_hits_pack.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp, vp]
     L.svo_hits_unpack.argtypes = [vp, C.POINTER(CastDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
@@ -509,6 +513,14 @@ class Tree:
         n = C.c_int64()
         _check(lib().svo_cast_blocks(C.byref(desc), C.byref(n)), "svo_cast_blocks")
         return n.value
+
+    @staticmethod
+    def cast_order(desc, wave_cost, wave_order, stream=None, group=1):
+        """wave_order (uint32 device tensor, svo_cast_blocks entries) = groups of `group` waves by
+        descending wave_cost (svo_cast_desc.wave_cost of a previous launch): longest first"""
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_cast_order(C.byref(desc), C.c_void_p(wave_cost.data_ptr()), group, C.c_void_p(wave_order.data_ptr()),
+                                    C.c_void_p(s) if s else None), "svo_cast_order")
 
     @staticmethod
     def alloc_hits(n, device, ao=False):
