@@ -453,7 +453,8 @@ def main():
             if ev is not None:
                 ev[0].record(stream)
             if args.shade:
-                tree.shade(desc, outs[b]["rgba"], out=outs[b], stream=stream, scene=scene)
+                # the image is the product: no hit records, so rays that provably leave the scene upwards stop early
+                tree.shade(desc, outs[b]["rgba"], out=None, stream=stream, scene=scene)
             else:
                 tree.cast(desc, outs[b], stream)
             if ev is not None:

@@ -76,6 +76,9 @@ struct CastParams {
     // frame mode dispatch order (svo_cast_desc.wave_order / wave_cost)
     const uint32_t* wave_order;
     uint32_t* wave_cost;
+    // shading: the highest stored voxel row of the scene / of the solid tree (tree_top_y); a ray
+    // moving up above it that cannot wrap in y before its budget ends can hit nothing more
+    int32_t top_scene, top_solid;
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
@@ -563,10 +566,13 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 
 // par_out: receives the parent of the region the ray ended in (it holds the final voxel; the LDS
 // path holds its ancestors at depths 0 .. levels-1-sh/2)
-template <bool STATS, bool REFLECT = false, class Mem>
+// ESCAPE (shading rays whose end position is not output): a ray moving up above the highest stored
+// voxel row `top` (wrapped) whose budget cannot carry it past the extent in y leaves the loop as a
+// miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off).
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
-                                     Bounce* bounce = nullptr, Parent* par_out = nullptr) {
+                                     Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -600,11 +606,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // one back-edge: every path through the body ends at the loop latch
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
+    bool escaped = false;
     while (!done) {
         // the voxel just entered is untested
         if (STATS) st.wv_iters += wave_lead();
         uint32_t w[3];
         wrap3(R, wm, w);
+        if (ESCAPE && top >= 0 && R.s[1] > 0 && (int32_t)w[1] > top && (int64_t)w[1] + R.steps <= (int64_t)wm) {
+            escaped = true;  // only empty voxels ahead: a miss
+            break;
+        }
         uint32_t sh = 0u;
         bool pend = false;  // the lookup found a brick: step through it below
         const uint32_t ax = R.axis;
@@ -761,7 +772,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
     // whose budget ends in empty space take their last steps together).  Every other way out of
     // the loop without a hit has spent the budget.
-    if (!hit) {
+    if (!hit && !escaped) {
         while (R.steps > 0) {
             dda_step(R);
             if (STATS) st.plain_steps++;
@@ -1003,7 +1014,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<false, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn);
+        const Hit h = trace<false, true, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -1034,7 +1045,8 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                     // shadow ray towards the sun from the centre of lastPos, through empty and liquid
                     const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                          (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                    dark = (trace<false>(P, smem, P.smats, path, so, P.sun, P.shadow_steps).info & HIT_BIT) != 0u;
+                    dark = (trace<false, false, true>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
+                                .info & HIT_BIT) != 0u;
                 }
             }
             if (dark) c = make_float3(col.x * 0.3f * m[0], col.y * 0.3f * m[1], col.z * 0.3f * m[2]);
@@ -1430,6 +1442,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     P.snodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.smats = reinterpret_cast<const uint16_t*>(t->d_mats);
     P.time = sd->time;
+    P.top_scene = tree_top_y(sc);
+    P.top_solid = tree_top_y(t);
     P.rgba = reinterpret_cast<float4*>(rgba);
     for (int k = 0; k < 3; k++) {
         P.sun[k] = sd->sun_dir[k];

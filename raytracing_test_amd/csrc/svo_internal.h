@@ -65,9 +65,13 @@ struct svo_tree {
     std::vector<uint32_t> dirty_nodes;           // rewritten in place below synced_nodes
     bool palette_dirty = false, full_upload = false;
     uint64_t dev_node_cap = 0, dev_mat_cap = 0, dev_pal_n = 0;  // device allocations (elements)
+    // highest voxel row holding a stored voxel (tree_top_y; -1: empty tree), cached until an edit
+    mutable int32_t top_y = -1;
+    mutable bool top_valid = false;
 };
 
 namespace svo {
+int32_t tree_top_y(const svo_tree* t);  // svo_world.cpp
 void tree_release_device(svo_tree* t);  // svo_cast.hip
 // take over device arrays built on `device` (node_cap / mat_cap elements allocated, the host image
 // already equal to their first nodes.size() / mats.size() elements): svo_cast.hip

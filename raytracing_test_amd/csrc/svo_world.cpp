@@ -581,6 +581,7 @@ extern "C" int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* x
         t->palette = w->pal.m;  // the world's palette only grows: ids stay valid
         t->palette_dirty = true;
     }
+    t->top_valid = false;
     Emitter em{t, w, std::vector<uint8_t>(w->pal.m.size()), {}};
     for (size_t i = 0; i < em.solid.size(); i++) em.solid[i] = material_in_view(w->pal.m[i], t->view);
     const uint32_t mk = (1u << (2 * L)) - 1u;
@@ -972,6 +973,43 @@ extern "C" int svo_tree_get_block(const svo_tree* t, int32_t x, int32_t y, int32
     *out = svo_block{m.flags, m.color, m.meta};
     if (mid) *mid = mat;
     return SVO_OK;
+}
+
+// Highest y of any stored voxel (wrapped coordinates), by a descent that visits child slots from the
+// top y-row down and prunes regions that cannot beat the best found so far; cached on the tree.
+namespace {
+int32_t top_y_of(const svo_tree* t, uint32_t ni, int32_t y0, int depth, int32_t best) {
+    const Node& n = t->nodes[ni];
+    const int32_t size = 1 << (2 * (t->levels - depth));
+    if (y0 + size - 1 <= best) return best;
+    const uint32_t kind = node_kind(n.info);
+    if (kind == K_SOLID) return y0 + size - 1;
+    if (kind == K_BRICK) {
+        for (int ly = 3; ly >= 0; ly--)
+            if (n.mask & (0x000F000F000F000Full << (4 * ly))) return std::max(best, y0 + ly);
+        return best;
+    }
+    const int32_t cs = size >> 2;
+    for (int sy = 3; sy >= 0; sy--) {
+        if (y0 + (sy + 1) * cs - 1 <= best) break;
+        for (int sz = 0; sz < 4; sz++)
+            for (int sx = 0; sx < 4; sx++) {
+                const uint32_t sl = (uint32_t)((sz << 4) | (sy << 2) | sx);
+                if (!((n.mask >> sl) & 1ull)) continue;
+                const uint32_t ci = n.ref + (uint32_t)__builtin_popcountll(n.mask & ((1ull << sl) - 1ull));
+                best = top_y_of(t, ci, y0 + sy * cs, depth + 1, best);
+            }
+    }
+    return best;
+}
+}  // namespace
+
+int32_t svo::tree_top_y(const svo_tree* t) {
+    if (!t->top_valid) {
+        t->top_y = t->nodes.empty() ? -1 : top_y_of(t, 0, 0, 0, -1);
+        t->top_valid = true;
+    }
+    return t->top_y;
 }
 
 extern "C" int svo_tree_node_indices(const svo_tree* t, const int32_t* xyz, int64_t n, uint64_t* idx) {

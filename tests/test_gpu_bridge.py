@@ -23,6 +23,10 @@ def bridge_out(tmp_path_factory):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     assert os.path.exists(BIN), "bridge_test not built (raytracing_test_amd/build.py build_bridge_test)"
+    # a binary older than the ABI header or the library it links would pass structs of the wrong size
+    for dep in (os.path.join(ROOT, "include", "svo_rt.h"), os.path.join(ROOT, "bridge", "svo_bridge.cpp"),
+                os.path.join(ROOT, "tests", "bridge", "bridge_test.cpp")):
+        assert os.path.getmtime(BIN) >= os.path.getmtime(dep), "bridge_test is older than %s: rebuild (__graft_entry__.build())" % dep
     out = str(tmp_path_factory.mktemp("bridge") / "out.json")
     p = subprocess.run([BIN, out], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-2000:])

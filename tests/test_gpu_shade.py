@@ -216,3 +216,19 @@ def test_full_view_tree_is_not_castable(rt, lake_scene):
     """castRayFromCam semantics need the solid view: a full-view tree is refused, not silently cast"""
     with pytest.raises(RuntimeError):
         lake_scene.cast_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 16, 16, 300)
+
+
+@pytest.mark.parametrize("cam", range(len(LAKE_CAMERAS)))
+def test_shade_escape_is_exact(rt, gtree, lake_scene, cam):
+    """without hit records, shading rays moving up above the highest stored voxel row stop early (no
+    voxel can be hit any more, and none of the remaining steps wraps in y): the image equals the one
+    rendered with hit records (every ray walks its whole budget), bit for bit, at large budgets too"""
+    org, cd = LAKE_CAMERAS[cam]
+    cam_dir = rt.normalize(cd)
+    for S in (300, 5000):
+        full, _ = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir(), with_hits=True, scene=lake_scene, time=0.5)
+        fast = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir(), scene=lake_scene, time=0.5)
+        assert np.array_equal(full.cpu().numpy(), fast.cpu().numpy()), (cam, S)
+        f2, _ = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir(), with_hits=True)
+        g2 = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir())
+        assert np.array_equal(f2.cpu().numpy(), g2.cpu().numpy()), (cam, S)
