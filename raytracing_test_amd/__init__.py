@@ -172,9 +172,13 @@ def lib():
     L.svo_gen_world.argtypes = [vp, i32, i32]
     L.svo_world_node_count.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.svo_build.argtypes = [vp, C.POINTER(vp)]
-    L.svo_build_view.argtypes = [vp, i32, C.POINTER(vp)]
-    L.svo_build_terrain_view.argtypes = [i32, i32, i32, i32, i32, C.POINTER(vp)]
-    L.svo_build_terrain_gpu_view.argtypes = [i32, i32, i32, i32, i32, C.POINTER(vp)]
+    # (entry points newer than SVO_RT_VERSION 3 are bound only when present, so that A/B timing against
+    # library builds of earlier revisions (tools/build_variant.py) loads them through this module)
+    for name, at in (("svo_build_view", [vp, i32, C.POINTER(vp)]), ("svo_build_terrain_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
+                     ("svo_build_terrain_gpu_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
+                     ("svo_cast_order", [C.POINTER(CastDesc), vp, i32, vp, vp])):
+        if hasattr(L, name):
+            getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
     L.svo_tree_get_info.argtypes = [vp, C.POINTER(TreeInfo)]
     L.svo_tree_palette.argtypes = [vp, C.c_uint32, C.POINTER(Block)]
@@ -187,7 +191,6 @@ def lib():
     L.svo_tree_destroy.restype = None
     L.svo_cast_count.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
     L.svo_cast_blocks.argtypes = [C.POINTER(CastDesc), C.POINTER(C.c_int64)]
-    L.svo_cast_order.argtypes = [C.POINTER(CastDesc), vp, i32, vp, vp]
     L.svo_hits_pack.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp, vp]
     L.svo_hits_unpack.argtypes = [vp, C.POINTER(CastDesc), vp, C.POINTER(Hits), vp]
     L.svo_cast_rays.argtypes = [vp, C.POINTER(CastDesc), C.POINTER(Hits), vp]
@@ -364,7 +367,10 @@ class World:
     def build(self, view=VIEW_SOLID):
         """the linearised tree of this world: VIEW_SOLID for casts, VIEW_ALL (liquid stored) as a shading scene"""
         h = C.c_void_p()
-        _check(lib().svo_build_view(self._h, view, C.byref(h)), "svo_build_view")
+        if view == VIEW_SOLID:
+            _check(lib().svo_build(self._h, C.byref(h)), "svo_build")
+        else:
+            _check(lib().svo_build_view(self._h, view, C.byref(h)), "svo_build_view")
         return Tree(h)
 
 
@@ -390,7 +396,10 @@ class Tree:
     def terrain(cls, levels, width, length, nthreads=0, view=VIEW_SOLID):
         """genWorld's column formula over width x length columns, built without per-voxel putBlock."""
         h = C.c_void_p()
-        _check(lib().svo_build_terrain_view(levels, width, length, nthreads, view, C.byref(h)), "svo_build_terrain_view")
+        if view == VIEW_SOLID:
+            _check(lib().svo_build_terrain(levels, width, length, nthreads, C.byref(h)), "svo_build_terrain")
+        else:
+            _check(lib().svo_build_terrain_view(levels, width, length, nthreads, view, C.byref(h)), "svo_build_terrain_view")
         return cls(h)
 
     @classmethod
@@ -406,7 +415,10 @@ class Tree:
     def terrain_gpu(cls, levels, width, length, device=0, view=VIEW_SOLID):
         """svo_build_terrain on the GPU (noise + build in HBM): the tree comes back uploaded to `device`."""
         h = C.c_void_p()
-        _check(lib().svo_build_terrain_gpu_view(levels, width, length, device, view, C.byref(h)), "svo_build_terrain_gpu_view")
+        if view == VIEW_SOLID:
+            _check(lib().svo_build_terrain_gpu(levels, width, length, device, C.byref(h)), "svo_build_terrain_gpu")
+        else:
+            _check(lib().svo_build_terrain_gpu_view(levels, width, length, device, view, C.byref(h)), "svo_build_terrain_gpu_view")
         return cls(h)
 
     @classmethod

@@ -26,3 +26,6 @@ d g3_f2 3 29543 --steps 4 --warmup 1 --frames 2 --verify
 d g2_ao 2 29544 --steps 4 --warmup 1 --ao 16 --verify
 d g2_shade 2 29545 --steps 4 --warmup 1 --shade
 step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/prof.err
+step rocprof_c5 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c5.json 2> $OUT/prof_c5.err
+step rocprof_c4 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- python3 bench.py --ao 16 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c4.json 2> $OUT/prof_c4.err
+step rocprof_shade timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_shade -o run -- python3 bench.py --shade --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_shade.json 2> $OUT/prof_shade.err
