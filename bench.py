@@ -532,6 +532,9 @@ def main():
     if args.stats and rank == 0:
         print_stats(rt, tree, desc, outs[0], stream, torch)
 
+    if exch is not None:  # the RCCL communicator of the exchange goes before the process group's
+        torch.cuda.synchronize()
+        exch.close()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

@@ -1,0 +1,93 @@
+"""bench.py's host logic on CPU: the CPU-baseline thread rule and its report, the roofline object (the
+§8(d) model next to the committed counters, `bound` from the counters), and the torch exchange's
+all-to-all splits for any frames / ranks (each sender's split to a rank equals that rank's split from
+it).  No kernel launches."""
+import argparse
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _args(**kw):
+    a = dict(config="c3", ao=0, shade=False)
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_cpu_info_reports_cores_and_model(bench, monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    ci = bench.cpu_info()
+    for k in ("nproc", "affinity_cpus", "cgroup_quota_cpus", "cpu_model", "threads", "threads_rule"):
+        assert k in ci
+    assert ci["threads"] == min(3, ci["affinity_cpus"]) and "OMP_NUM_THREADS" in ci["threads_rule"]
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    ci = bench.cpu_info()
+    assert 1 <= ci["threads"] <= ci["affinity_cpus"] and ci["nproc"] >= ci["affinity_cpus"]
+
+
+def test_run_keys(bench):
+    assert bench.run_key(_args()) == "c3"
+    assert bench.run_key(_args(ao=16)) == "c3_ao16"
+    assert bench.run_key(_args(config="c5")) == "c5"
+    assert bench.run_key(_args(shade=True)) == "c3_shade"
+
+
+def test_roofline_model_and_counters(bench):
+    cfg = bench.CONFIGS["c3"]
+    bray = json.load(open(os.path.join(ROOT, "profiles", "bray.json")))
+    r = bench.roofline(_args(), cfg, 2073600, 0.23e-3, 1)
+    b = bray["C3"]["bytes_per_ray"]
+    assert abs(r["bytes_per_ray"] - b) < 0.01
+    assert abs(r["achieved"] - b * 2073600 / 0.23e-3 / 1e9) < 0.01
+    assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-4
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_c3.json")))
+    assert r["traffic"] == round(pmc["hbm_bytes_per_launch"])  # the same rays per launch: unscaled
+    assert r["bound"] == ("valu-issue" if r["valu_issue_frac"] > r["hbm_frac_measured"] else "hbm")
+    # C4 prices the AO rays' node entries too; a shaded line has no §8(d) model
+    r4 = bench.roofline(_args(ao=16), cfg, 2073600, 0.31e-3, 1)
+    assert abs(r4["bytes_per_ray"] - bray["C4_ao16"]["bytes_per_ray"]) < 0.01 and r4["bytes_per_ray"] > r["bytes_per_ray"]
+    rs = bench.roofline(_args(shade=True), cfg, 2073600, 1.3e-3, 1)
+    assert rs["frac"] is None and rs["bytes_per_ray"] is None
+    # counters measured at N = 1 scale per ray to another launch size (a rank's shard)
+    rh = bench.roofline(_args(), cfg, 2073600 // 2, 0.12e-3, 2)
+    assert rh["traffic"] == round(pmc["hbm_bytes_per_launch"] / 2)
+
+
+@pytest.mark.parametrize("world,nframes", [(1, 1), (2, 1), (2, 2), (3, 2), (3, 5), (4, 4), (8, 8), (8, 1)])
+def test_torch_exchange_splits_pair_up(bench, world, nframes):
+    from raytracing_test_amd import shard
+
+    W, H = 64, 37
+    counts = [shard.shard_count(W, H, r, world) for r in range(world)]
+    send, recv = {}, {}
+    for rank in range(world):
+        x = bench.TorchExchange.__new__(bench.TorchExchange)
+        x.world, x.rank, x.counts, x.n_mine, x.nframes = world, rank, counts, counts[rank], nframes
+        x.mine = list(range(rank, nframes, world))
+        send[rank], recv[rank] = x._splits(1)
+        # the regrouped send buffer: frames grouped by destination rank (frames r, r + N, ...), each once
+        import torch
+
+        x.torch = torch
+        buf = torch.arange(counts[rank] * nframes)
+        got = x._order_send(buf).numpy()
+        want = np.concatenate([np.arange(f * counts[rank], (f + 1) * counts[rank]) for r in range(world) for f in range(r, nframes, world)])
+        assert np.array_equal(got, want)
+        assert sum(send[rank]) == counts[rank] * nframes
+        assert sum(recv[rank]) == len(x.mine) * W * H
+    for s in range(world):
+        for r in range(world):
+            assert send[s][r] == recv[r][s], (s, r)
