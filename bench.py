@@ -287,6 +287,10 @@ def main():
                          "(svo_cast_desc.wave_cost) and svo_cast_order sorts them, longest first, on a side stream for the launch "
                          "after next; sync = the same on the launch stream for the next launch; none = top tile rows first")
     ap.add_argument("--order-group", type=int, default=16, help="svo_cast_order: waves per group kept together")
+    ap.add_argument("--pipelined-steps", type=int, default=None,
+                    help="N = 1: after the timed region, time this many more steps with consecutive launches on two "
+                         "alternating streams (a launch's tail overlaps the next one's head), reported as `pipelined` "
+                         "(default: --steps; 0: off)")
     ap.add_argument("--launch-events", action="store_true",
                     help="an event pair around every cast launch (default at N=1: one pair around the timed region, whose "
                          "average per launch includes the gaps between launches; per-launch pairs cost ~7 us per step)")
@@ -369,14 +373,18 @@ def main():
     if gather:
         xmode = "torch" if (args.shade or args.exchange == "torch" or args.dist_backend != "nccl") else "capi"
     gdev = torch.device("cuda", dev)
-    nbuf = 2 if gather else 1  # the exchange of step k overlaps the cast of step k+1
+    pipe_steps = args.steps if args.pipelined_steps is None else args.pipelined_steps
+    if gather or args.order != "none" or world > 1:
+        pipe_steps = 0  # (an N = 1 measurement beside the contract's own)
+    nbuf = 2 if (gather or pipe_steps) else 1  # the exchange (or the next launch) of step k overlaps step k+1
     outs = []
     for _ in range(nbuf):
         views = rt.Tree.alloc_hits(rays_per_launch, dev, ao=args.ao > 0)
         if args.shade:
             views["rgba"] = torch.zeros((rays_per_launch, 4), dtype=torch.float32, device=gdev)
         outs.append(views)
-    stream = torch.cuda.Stream(device=dev)
+    cstreams = [torch.cuda.Stream(device=dev) for _ in range(2 if pipe_steps else 1)]
+    stream = cstreams[0]
     xstream = torch.cuda.Stream(device=dev) if gather else None
     exch = None
     xnote = None
@@ -444,8 +452,9 @@ def main():
             rt.Tree.cast_order(desc, ocost[0], oorder[0], stream, group=args.order_group)
         ovalid[j] = True
 
-    def one_step(k, ev=None):
+    def one_step(k, ev=None, pipe=False):
         b = k % nbuf
+        stream = cstreams[k % 2] if pipe else cstreams[0]
         with torch.cuda.stream(stream):
             if xdone[b] is not None:
                 stream.wait_event(xdone[b])  # the exchange that read this buffer set has passed
@@ -512,6 +521,30 @@ def main():
     total_rays = W * H * nframes * args.steps  # every rank's share of every frame, all steps
     value = total_rays / elapsed
     avg_kernel_s = float(np.mean(kern_ms)) / 1e3
+    pipelined = None
+    if pipe_steps:
+        # the same steps with consecutive launches on two alternating streams: frames are independent, so a
+        # renderer keeps two in flight and the next launch's long waves fill this one's tail
+        for _ in range(max(2, args.warmup)):  # (the second stream's first launches set up its queue)
+            one_step(step_no, None, pipe=True)
+            step_no += 1
+        torch.cuda.synchronize()
+        pe = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        tp = time.perf_counter()
+        pe[0].record(cstreams[0])
+        cstreams[1].wait_event(pe[0])
+        for k in range(pipe_steps):
+            one_step(step_no, None, pipe=True)
+            step_no += 1
+        pe[1].record(cstreams[1])
+        cstreams[0].wait_event(pe[1])
+        pe[2].record(cstreams[0])
+        torch.cuda.synchronize()
+        tp = time.perf_counter() - tp
+        pipelined = {"value": round(W * H * nframes * pipe_steps / tp, 1), "ms_per_step": round(tp / pipe_steps * 1e3, 4),
+                     "event_ms_per_step": round(pe[0].elapsed_time(pe[2]) / pipe_steps, 4), "steps": pipe_steps,
+                     "how": "consecutive launches alternate between two streams (two frames in flight); each launch "
+                            "itself runs longer, sharing the GPU: the per-launch roofline above is the one-at-a-time figure"}
 
     verified = None
     if args.verify and gather and not args.shade:
@@ -589,6 +622,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         **({"gather_verified": verified} if verified is not None else {}),
+        **({"pipelined": pipelined} if pipelined is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
                          "included)" if region_events else "a HIP event pair around every launch on its stream",
     }
