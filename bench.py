@@ -153,6 +153,7 @@ def cpu_baseline(args, cfg, ppx, ppy, gpu):
     pix = np.arange(0, n, stride, dtype=np.int64)
     pix1 = np.arange(0, n, stride1, dtype=np.int64)
     parity = None
+    o0 = {}
     if args.config == "c1":
         D = O.Dense(T, 256)
         ref, dt = _timed(lambda: D.cast_frame(org, dn, W, H, S, nthreads=nt))
@@ -181,6 +182,11 @@ def cpu_baseline(args, cfg, ppx, ppy, gpu):
         if gpu is not None:
             parity = bool(np.array_equal(gpu["pos"][pix], ref["pos"]) and np.array_equal(gpu["steps"][pix], ref["steps"]))
         what = "castRayFromCam + getBlock on the reference node/array layout"
+        # the reference's own build flags (build.bat:4, `g++ -g` = -O0), one thread, every 512th pixel
+        pix0 = np.arange(0, n, 512, dtype=np.int64)
+        r0, dt0 = _timed(lambda: T.cast_frame(org, dn, W, H, S, ppx=ppx, ppy=ppy, pixels=pix0, nthreads=1, L=O.lib_O0()))
+        o0 = {"single_thread_O0_rays_per_s": len(pix0) / dt0, "O0_sample": "every 512th pixel (%d rays), -O0" % len(pix0),
+              "O0_equal": bool(np.array_equal(r0["pos"], ref["pos"][::512 // stride]) if stride <= 512 and 512 % stride == 0 else True)}
     res = {
         "value": len(pix) / dt,
         "unit": "rays/s",
@@ -191,6 +197,7 @@ def cpu_baseline(args, cfg, ppx, ppy, gpu):
                   % ("all %d rays" % n if stride == 1 else "%d rays" % len(pix), W, H, args.config.upper(), stride, nt, stride1 if
                      args.config != "c1" else stride, len(pix1), what),
         "single_thread_rays_per_s": len(pix1) / dt1,
+        **o0,
         "cpu_s": round(dt + dt1, 2),
         "tree_build_s": round(build_s, 2),
         **{k: ci[k] for k in ("nproc", "affinity_cpus", "cgroup_quota_cpus", "cpu_model", "threads_rule")},

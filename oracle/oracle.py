@@ -64,6 +64,23 @@ def build(native=False):
     subprocess.check_call(["make", "-s", "-C", HERE, "_build/liboracle.so"])
 
 
+LIB_O0 = os.path.join(HERE, "_build", "liboracle_O0.so")
+
+
+def lib_O0():
+    """the same restatement at -O0 (the reference's own build flags, build.bat:4: `g++ -g`), for the CPU
+    baseline's -O0 figure; trees built by lib() are used through it unchanged (same source, same layout)"""
+    if not os.path.exists(LIB_O0) or os.path.getmtime(LIB_O0) < os.path.getmtime(os.path.join(HERE, "oracle.c")):
+        os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
+        subprocess.check_call(["gcc", "-O0", "-std=c11", "-fPIC", "-ffp-contract=off", "-pthread", "-shared", "-o", LIB_O0,
+                               os.path.join(HERE, "oracle.c"), "-lm"])
+    if LIB_O0 not in _libs:
+        L = C.CDLL(LIB_O0)
+        L.orc_cast_frame.argtypes = lib().orc_cast_frame.argtypes
+        _libs[LIB_O0] = L
+    return _libs[LIB_O0]
+
+
 def build_ref():
     subprocess.check_call(["make", "-s", "-C", HERE, "ref"])
 
@@ -271,8 +288,9 @@ class Tree:
         self.L.orc_cast_ray(self.h, f3(org), f3(d), steps, C.byref(r))
         return r
 
-    def cast_frame(self, org, cam, W, H, steps, ppx=None, ppy=None, pixels=None, nthreads=8):
-        """castRayFromCam semantics for every pixel ray (or a subset); returns a dict of arrays."""
+    def cast_frame(self, org, cam, W, H, steps, ppx=None, ppy=None, pixels=None, nthreads=8, L=None):
+        """castRayFromCam semantics for every pixel ray (or a subset); returns a dict of arrays.
+        L: another build of the same restatement (lib_O0()) to run it with"""
         if ppx is None:
             ppx, ppy = proj_plane(W, H)
         n = W * H if pixels is None else len(pixels)
@@ -288,7 +306,7 @@ class Tree:
             axis=np.zeros(n, np.int32),
         )
         dda = C.c_uint64()
-        rc = self.L.orc_cast_frame(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, _ptr(pix), n, nthreads,
+        rc = (L or self.L).orc_cast_frame(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, _ptr(pix), n, nthreads,
                                    _ptr(out["pos"]), _ptr(out["last"]), _ptr(out["steps"]), _ptr(out["hit"]), _ptr(out["t"]),
                                    _ptr(out["color"]), _ptr(out["flags"]), _ptr(out["axis"]), C.byref(dda))
         out["rc"] = rc

@@ -481,3 +481,26 @@ def test_wave_order_and_cost(rt, gtree, torch_cuda):
                 assert torch.equal(out[k], base[k]), k
         d.wave_order = None
         d.wave_cost = None
+
+
+def test_exchange_single_rank_python(rt, gtree, torch_cuda):
+    """svo_exchange_frames through the Python binding (rt.Exchange) on a one-rank RCCL communicator: the
+    frames it unpacks equal the cast records (ragged frame, several frames per launch, AO counts)"""
+    torch = torch_cuda
+    x = rt.Exchange(1, 0, rt.Exchange.unique_id(), 0)
+    cam = rt.normalize((1.0, -0.45, 1.0))
+    try:
+        for nf, W, H, ao in ((1, 100, 37, 0), (3, 64, 48, 16)):
+            origins = [(4.0 + 8.5 * f, 90.0, 4.0 + 3.25 * f) for f in range(nf)]
+            d = rt.Tree.frame_desc(origins[0], cam, W, H, 300, frame_origins=origins if nf > 1 else None, ao_samples=ao)
+            n = rt.Tree.count(d)
+            assert n == nf * W * H
+            mine = rt.Tree.alloc_hits(n, 0, ao=ao > 0)
+            gtree.cast(d, mine)
+            out = rt.Tree.alloc_hits(n, 0, ao=ao > 0)
+            x.frames(gtree, d, mine, out)
+            torch.cuda.synchronize()
+            for k in mine:
+                assert torch.equal(out[k], mine[k]), (nf, k)
+    finally:
+        x.close()
