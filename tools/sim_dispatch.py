@@ -50,3 +50,10 @@ for g in (2, 4, 8, 16, 30, 60, 120):
         ordr = np.argsort(-key, kind="stable")
         order = (ordr[:, None] * g + np.arange(g)[None, :]).reshape(-1)
         print("sim LPT groups of %d by %s: %.1f" % (g, nm, sim(order)[0]))
+# hybrid: the heaviest fraction of waves first (longest first), the rest in the shipped order
+for frac in (0.01, 0.02, 0.05, 0.1, 0.2):
+    k = int(n * frac)
+    heavy = np.argsort(-dur, kind="stable")[:k]
+    mask = np.ones(n, bool); mask[heavy] = False
+    order = np.concatenate([heavy, np.arange(n)[mask]])
+    print("sim heaviest %4.1f%% first: %.1f" % (100 * frac, sim(order)[0]))
