@@ -23,9 +23,10 @@
 extern "C" {
 #endif
 
-#define SVO_RT_VERSION 5  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
+#define SVO_RT_VERSION 6  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
                              4: tree views (liquid stored for the shading pass), svo_shade_desc.scene / time;
-                             5: svo_cast_desc.wave_order / wave_cost + svo_cast_order (cost-ordered dispatch) */
+                             5: svo_cast_desc.wave_order / wave_cost + svo_cast_order (cost-ordered dispatch);
+                             6: svo_tree_save / svo_tree_load */
 
 enum {
     SVO_OK = 0,
@@ -33,7 +34,8 @@ enum {
     SVO_ENOMEM = -2,  /* host or device allocation failed */
     SVO_EDEVICE = -3, /* HIP runtime error / no GPU */
     SVO_ESTATE = -4,  /* object not in the required state (e.g. tree not uploaded) */
-    SVO_ERANGE = -5   /* value outside what the structure supports */
+    SVO_ERANGE = -5,  /* value outside what the structure supports */
+    SVO_EIO = -6      /* file I/O failed, or the file is not a valid tree (svo_tree_load) */
 };
 
 /* Block (src/globals.hpp:76-80): leaf flags (bit 0 set for a stored voxel; REFLECTIVE 0x2,
@@ -154,6 +156,12 @@ int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* xyz, int64_t
    after a rebuild / when the device allocation is outgrown) */
 int svo_tree_sync(svo_tree* t);
 void svo_tree_destroy(svo_tree* t);
+/* Checkpoint (the reference regenerates its world at every start, main.cpp:190): write the
+   linearised tree (levels, view, palette, nodes, material runs; a checksum) to `path`, and read it back
+   as a new tree (not uploaded).  Loading validates every child / material reference against the array
+   sizes, so a damaged file fails with SVO_EIO instead of reaching a kernel. */
+int svo_tree_save(const svo_tree* t, const char* path);
+int svo_tree_load(const char* path, svo_tree** out);
 
 /* ---------------------------------------------------------------------------- casting ------- */
 /* Hit record per ray (caller-owned device buffers, 24 B / ray):

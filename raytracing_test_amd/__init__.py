@@ -140,7 +140,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
-    "svo_cast_order",
+    "svo_cast_order", "svo_tree_save", "svo_tree_load",
 )
 
 
@@ -176,7 +176,8 @@ def lib():
     # library builds of earlier revisions (tools/build_variant.py) loads them through this module)
     for name, at in (("svo_build_view", [vp, i32, C.POINTER(vp)]), ("svo_build_terrain_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
                      ("svo_build_terrain_gpu_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
-                     ("svo_cast_order", [C.POINTER(CastDesc), vp, i32, vp, vp])):
+                     ("svo_cast_order", [C.POINTER(CastDesc), vp, i32, vp, vp]),
+                     ("svo_tree_save", [vp, C.c_char_p]), ("svo_tree_load", [C.c_char_p, C.POINTER(vp)])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -428,6 +429,17 @@ class Tree:
         _check(lib().svo_build_heightfield_gpu(levels, h.shape[0], h.shape[1], h.ctypes.data_as(C.c_void_p), device, C.byref(t)),
                "svo_build_heightfield_gpu")
         return cls(t)
+
+    def save(self, path):
+        """checkpoint the linearised tree to a file (svo_tree_save)"""
+        _check(lib().svo_tree_save(self._h, os.fsencode(path)), "svo_tree_save")
+
+    @classmethod
+    def load(cls, path):
+        """a tree read back from svo_tree_save's file (validated; not uploaded)"""
+        h = C.c_void_p()
+        _check(lib().svo_tree_load(os.fsencode(path), C.byref(h)), "svo_tree_load")
+        return cls(h)
 
     def info(self):
         i = TreeInfo()

@@ -8,6 +8,7 @@
 // Both emit the same canonical form (tests check they agree node for node), defined in
 // svo_common.h.  Reference paths are relative to the reedthorngag/raytracing_test snapshot.
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -16,6 +17,7 @@
 #include <functional>
 #include <unordered_map>
 #include <map>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -1040,6 +1042,143 @@ extern "C" int svo_tree_export(const svo_tree* t, void* nodes, uint64_t nb, void
         if (mb < t->mats.size() * sizeof(uint16_t)) SVO_FAIL(SVO_ERANGE, "svo_tree_export: material buffer too small");
         memcpy(mats, t->mats.data(), t->mats.size() * sizeof(uint16_t));
     }
+    return SVO_OK;
+}
+
+// ================================================================================================
+// Checkpoint: svo_tree_save / svo_tree_load
+//   header  "SVOTREE1" | u32 format 1 | i32 levels | i32 view | u32 n_palette | u64 n_nodes | u64 n_mats |
+//           u64 n_bricks | u64 nodes_per_level[8]
+//   palette n_palette x {u32 flags, u32 0, u64 color, f32 meta, u32 0}
+//   nodes   n_nodes x 16 B, mats n_mats x 2 B, then u64 FNV-1a of everything before it
+// ================================================================================================
+namespace {
+struct Fnv {
+    uint64_t h = 1469598103934665603ull;
+    void add(const void* p, size_t n) {
+        const uint8_t* b = static_cast<const uint8_t*>(p);
+        for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    }
+};
+struct FileOut {
+    FILE* f;
+    Fnv sum;
+    bool ok = true;
+    void put(const void* p, size_t n) {
+        if (n && fwrite(p, 1, n, f) != n) ok = false;
+        sum.add(p, n);
+    }
+};
+struct FileIn {
+    FILE* f;
+    Fnv sum;
+    bool get(void* p, size_t n) {
+        if (n && fread(p, 1, n, f) != n) return false;
+        sum.add(p, n);
+        return true;
+    }
+};
+const char kMagic[8] = {'S', 'V', 'O', 'T', 'R', 'E', 'E', '1'};
+}  // namespace
+
+extern "C" int svo_tree_save(const svo_tree* t, const char* path) {
+    if (!t || !path) SVO_FAIL(SVO_EINVAL, "svo_tree_save: NULL argument");
+    FileOut o{fopen(path, "wb")};
+    if (!o.f) SVO_FAIL(SVO_EIO, std::string("svo_tree_save: cannot open ") + path);
+    const uint32_t fmt = 1, npal = (uint32_t)t->palette.size();
+    const uint64_t nn = t->nodes.size(), nm = t->mats.size(), nb = t->n_bricks;
+    o.put(kMagic, 8);
+    o.put(&fmt, 4);
+    o.put(&t->levels, 4);
+    o.put(&t->view, 4);
+    o.put(&npal, 4);
+    o.put(&nn, 8);
+    o.put(&nm, 8);
+    o.put(&nb, 8);
+    o.put(t->nodes_per_level, sizeof(t->nodes_per_level));
+    for (const Material& m : t->palette) {
+        const uint32_t z = 0;
+        o.put(&m.flags, 4);
+        o.put(&z, 4);
+        o.put(&m.color, 8);
+        o.put(&m.meta, 4);
+        o.put(&z, 4);
+    }
+    o.put(t->nodes.data(), nn * sizeof(Node));
+    o.put(t->mats.data(), nm * sizeof(uint16_t));
+    const uint64_t h = o.sum.h;
+    o.put(&h, 8);
+    const bool closed = fclose(o.f) == 0;
+    if (!o.ok || !closed) SVO_FAIL(SVO_EIO, std::string("svo_tree_save: write failed: ") + path);
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_load(const char* path, svo_tree** out) {
+    if (!path || !out) SVO_FAIL(SVO_EINVAL, "svo_tree_load: NULL argument");
+    *out = nullptr;
+    FileIn in{fopen(path, "rb")};
+    if (!in.f) SVO_FAIL(SVO_EIO, std::string("svo_tree_load: cannot open ") + path);
+    struct Closer {
+        FILE* f;
+        ~Closer() { fclose(f); }
+    } closer{in.f};
+    char magic[8];
+    uint32_t fmt = 0, npal = 0;
+    int32_t levels = 0, view = 0;
+    uint64_t nn = 0, nm = 0, nb = 0, per[8];
+    if (!in.get(magic, 8) || memcmp(magic, kMagic, 8) != 0) SVO_FAIL(SVO_EIO, "svo_tree_load: not a tree file");
+    if (!in.get(&fmt, 4) || fmt != 1) SVO_FAIL(SVO_EIO, "svo_tree_load: unknown format");
+    if (!in.get(&levels, 4) || !in.get(&view, 4) || !in.get(&npal, 4) || !in.get(&nn, 8) || !in.get(&nm, 8) || !in.get(&nb, 8) ||
+        !in.get(per, sizeof(per)))
+        SVO_FAIL(SVO_EIO, "svo_tree_load: truncated header");
+    if (levels < 1 || levels > 7 || (view != SVO_VIEW_SOLID && view != SVO_VIEW_ALL) || npal < 1 || npal > 0xFFFFu || nn < 1 ||
+        nn > 0xFFFFFFFFull || nm > 0xFFFFFFFFull)
+        SVO_FAIL(SVO_EIO, "svo_tree_load: header out of range");
+    std::unique_ptr<svo_tree> t(new (std::nothrow) svo_tree());
+    if (!t) SVO_FAIL(SVO_ENOMEM, "svo_tree_load: out of memory");
+    t->levels = levels;
+    t->view = view;
+    t->n_bricks = nb;
+    memcpy(t->nodes_per_level, per, sizeof(per));
+    t->palette.resize(npal);
+    for (Material& m : t->palette) {
+        uint32_t z0, z1;
+        if (!in.get(&m.flags, 4) || !in.get(&z0, 4) || !in.get(&m.color, 8) || !in.get(&m.meta, 4) || !in.get(&z1, 4))
+            SVO_FAIL(SVO_EIO, "svo_tree_load: truncated palette");
+    }
+    try {
+        t->nodes.resize(nn);
+        t->mats.resize(nm);
+    } catch (...) {
+        SVO_FAIL(SVO_ENOMEM, "svo_tree_load: out of memory");
+    }
+    if (!in.get(t->nodes.data(), nn * sizeof(Node)) || !in.get(t->mats.data(), nm * sizeof(uint16_t)))
+        SVO_FAIL(SVO_EIO, "svo_tree_load: truncated arrays");
+    const uint64_t want = in.sum.h;
+    uint64_t h = 0;
+    if (fread(&h, 1, 8, in.f) != 8 || h != want) SVO_FAIL(SVO_EIO, "svo_tree_load: checksum mismatch");
+    // every reference inside the arrays: what the kernels will follow
+    for (uint64_t i = 0; i < nn; i++) {
+        const Node& n = t->nodes[i];
+        const uint32_t kind = node_kind(n.info);
+        const uint64_t cnt = (uint64_t)__builtin_popcountll(n.mask);
+        if (kind == K_INTERIOR) {
+            if (cnt && ((uint64_t)n.ref + cnt > nn || n.ref == 0)) SVO_FAIL(SVO_EIO, "svo_tree_load: child reference out of range");
+        } else if (kind == K_BRICK) {
+            if (n.info & K_UNIFORM) {
+                if (node_material(n.info) >= npal) SVO_FAIL(SVO_EIO, "svo_tree_load: material out of range");
+            } else if ((uint64_t)n.ref + cnt > nm) {
+                SVO_FAIL(SVO_EIO, "svo_tree_load: material run out of range");
+            }
+        } else if (kind == K_SOLID) {
+            if (node_material(n.info) >= npal) SVO_FAIL(SVO_EIO, "svo_tree_load: material out of range");
+        } else {
+            SVO_FAIL(SVO_EIO, "svo_tree_load: unknown node kind");
+        }
+    }
+    for (uint64_t i = 0; i < nm; i++)
+        if (t->mats[i] >= npal) SVO_FAIL(SVO_EIO, "svo_tree_load: material out of range");
+    *out = t.release();
     return SVO_OK;
 }
 

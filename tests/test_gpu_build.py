@@ -58,3 +58,16 @@ def test_terrain_gpu_casts_and_c3_build_time(rt, torch_cuda):
     for k in ("pos_steps", "t", "info"):
         assert torch_cuda.equal(a[k], b[k]), k
     print("C3 GPU build %.3f s" % dt)
+
+
+def test_checkpoint_of_gpu_tree_casts_the_same(rt, torch_cuda, tmp_path):
+    """a GPU-built tree saved (svo_tree_save) and loaded back (svo_tree_load) casts bit for bit like the
+    original once uploaded (the checkpoint replaces a rebuild at start-up)"""
+    g = rt.Tree.terrain_gpu(6, 2048, 2048, 0)
+    p = str(tmp_path / "c3.svo")
+    g.save(p)
+    h = rt.Tree.load(p).upload(0)
+    cam = rt.normalize((1.0, -0.45, 1.0))
+    a, b = g.cast_frame((4.0, 90.0, 4.0), cam, 640, 360, 16384), h.cast_frame((4.0, 90.0, 4.0), cam, 640, 360, 16384)
+    for k in ("pos_steps", "t", "info"):
+        assert torch_cuda.equal(a[k], b[k]), k
