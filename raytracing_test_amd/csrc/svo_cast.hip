@@ -1291,12 +1291,12 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_nodes) (void)hipFree(t->d_nodes);
     if (t->d_mats) (void)hipFree(t->d_mats);
     if (t->d_pal) (void)hipFree(t->d_pal);
-    if (t->d_work) (void)hipFree(t->d_work);
+    if (t->d_pick) (void)hipFree(t->d_pick);
     if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
     t->d_ao_plan = nullptr;
     t->ao_plan_steps = -1;
     (void)hipSetDevice(prev);
-    t->d_nodes = t->d_mats = t->d_work = t->d_pal = nullptr;
+    t->d_nodes = t->d_mats = t->d_pick = t->d_pal = nullptr;
     t->dev_node_cap = t->dev_mat_cap = t->dev_pal_n = 0;
     t->device = -1;
     t->device_bytes = 0;
@@ -1340,16 +1340,14 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     const size_t wb = 4096;
     HIP_TRY(hipMalloc(&t->d_nodes, nb), SVO_ENOMEM);
     HIP_TRY(hipMalloc(&t->d_mats, mb), SVO_ENOMEM);
-    HIP_TRY(hipMalloc(&t->d_work, wb), SVO_ENOMEM);
+    HIP_TRY(hipMalloc(&t->d_pick, wb), SVO_ENOMEM);
     HIP_TRY(hipMemcpy(t->d_nodes, t->nodes.data(), t->nodes.size() * sizeof(Node), hipMemcpyHostToDevice), SVO_EDEVICE);
     if (!t->mats.empty()) HIP_TRY(hipMemcpy(t->d_mats, t->mats.data(), t->mats.size() * sizeof(uint16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
-    HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
+    HIP_TRY(hipMemset(t->d_pick, 0, wb), SVO_EDEVICE);
     int rc = upload_palette(t);
     if (rc) return rc;
     t->device = device;
     t->device_bytes = nb + mb + wb + t->dev_pal_n * 12;
-    t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
-    t->work_next = 0;
     t->dev_node_cap = ncap;
     t->dev_mat_cap = mcap;
     t->synced_nodes = t->nodes.size();
@@ -1365,14 +1363,12 @@ int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_
     const size_t wb = 4096;
     t->d_nodes = d_nodes;
     t->d_mats = d_mats;
-    HIP_TRY(hipMalloc(&t->d_work, wb), SVO_ENOMEM);
-    HIP_TRY(hipMemset(t->d_work, 0, wb), SVO_EDEVICE);
+    HIP_TRY(hipMalloc(&t->d_pick, wb), SVO_ENOMEM);
+    HIP_TRY(hipMemset(t->d_pick, 0, wb), SVO_EDEVICE);
     int rc = upload_palette(t);
     if (rc) return rc;
     t->device = device;
     t->device_bytes = node_cap * sizeof(Node) + mat_cap * sizeof(uint16_t) + wb + t->dev_pal_n * 12;
-    t->work_slots = (uint32_t)(wb / sizeof(uint32_t));
-    t->work_next = 0;
     t->dev_node_cap = node_cap;
     t->dev_mat_cap = mat_cap;
     t->synced_nodes = t->nodes.size();
@@ -1509,7 +1505,10 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     if (steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: negative step budget");
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     void* buf = nullptr;
-    HIP_TRY(hipMalloc(&buf, 64), SVO_ENOMEM);
+    // the tree's own 64-B result record: no allocation per pick (the reference casts one every frame,
+    // main.cpp:81); one pick at a time per tree
+    std::lock_guard<std::mutex> lock(t->pick_mu);
+    buf = t->d_pick;
     CastParams P;
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
@@ -1528,7 +1527,6 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     launch_cast<false, false, false, false>(wide_nodes(t, 0), dim3(1), dim3(kBlock), nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
-    (void)hipFree(buf);
     if (e != hipSuccess) SVO_FAIL(SVO_EDEVICE, std::string("svo_cast_ray_from_cam: ") + hipGetErrorString(e));
     int32_t p4[4];
     uint32_t info;

@@ -4,6 +4,7 @@
 
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -50,13 +51,12 @@ struct svo_tree {
     int32_t device = -1;
     void* d_nodes = nullptr;
     void* d_mats = nullptr;
-    void* d_work = nullptr;   // scheduler counters (ring)
+    void* d_pick = nullptr;   // the pick ray's result record (svo_cast_ray_from_cam), 64 B
     void* d_pal = nullptr;    // palette for shading: u64 colour[n] then u32 flags[n]
     // hemisphere AO plan (svo_cast.hip, built on first use for (ao_samples, ao_steps))
     mutable void* d_ao_plan = nullptr;
     mutable int32_t ao_plan_n = 0, ao_plan_steps = -1;
-    uint32_t work_slots = 0;
-    uint32_t work_next = 0;
+    mutable std::mutex pick_mu;  // one pick ray at a time per tree (d_pick)
     uint64_t device_bytes = 0;
     // incremental edits (svo_tree_update in svo_world.cpp, svo_tree_sync in svo_cast.hip): changed
     // node blocks are appended; superseded ones are garbage until the next full rebuild

@@ -504,3 +504,18 @@ def test_exchange_single_rank_python(rt, gtree, torch_cuda):
                 assert torch.equal(out[k], mine[k]), (nf, k)
     finally:
         x.close()
+
+
+def test_pick_ray_repeated(rt, gtree):
+    """the per-frame pick ray (main.cpp:81: castRayFromCam(30) every frame, svo_cast_ray_from_cam) uses the
+    tree's own result record: repeated picks agree, and one costs well under a millisecond"""
+    import time
+
+    cam = rt.normalize((1.0, 0.0, 1.0))
+    first = gtree.cast_ray_from_cam((35.0, 50.0, 35.0), cam, 30)
+    t0 = time.perf_counter()
+    for _ in range(200):
+        assert gtree.cast_ray_from_cam((35.0, 50.0, 35.0), cam, 30) == first
+    dt = (time.perf_counter() - t0) / 200
+    print("pick ray: %.1f us per call" % (dt * 1e6))
+    assert dt < 1e-3
