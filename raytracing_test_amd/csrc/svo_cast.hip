@@ -76,6 +76,7 @@ struct CastParams {
     // frame mode dispatch order (svo_cast_desc.wave_order / wave_cost)
     const uint32_t* wave_order;
     uint32_t* wave_cost;
+    uint32_t n_waves;  // waves of the launch (a wave_order entry at or beyond it casts nothing)
     // shading: the highest stored voxel row of the scene / of the solid tree (tree_top_y); a ray
     // moving up above it that cannot wrap in y before its budget ends can hit nothing more
     int32_t top_scene, top_solid;
@@ -967,13 +968,14 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         // the previous launch's costs) permutes the waves over the launch's blocks.
         wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         if (P.wave_order) wv = __builtin_amdgcn_readfirstlane(P.wave_order[wv]);
+        if (wv >= P.n_waves) wv = P.n_waves;  // a malformed order: this block casts nothing (and records nothing)
         const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
         const int32_t lane = (int32_t)(threadIdx.x & 63u);
         const uint32_t tq = tile / (uint32_t)P.tiles_x;
         int32_t trl = (int32_t)tq;
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
-        if (P.use_row_order) trl = P.row_order[tq];
+        if (P.use_row_order) trl = tq < (uint32_t)kMaxOrderRows ? P.row_order[tq] : -1;
         else if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
@@ -982,7 +984,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
         const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
         const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+        if (wv < P.n_waves && trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
             o[0] = P.frame_org[3 * fr + 0];
             o[1] = P.frame_org[3 * fr + 1];
@@ -1083,7 +1085,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
             P.ao[out] = (uint8_t)cnt;
         }
     }
-    if (P.wave_cost && P.mode == MODE_FRAME && (threadIdx.x & 63u) == 0u)
+    if (P.wave_cost && P.mode == MODE_FRAME && wv < P.n_waves && (threadIdx.x & 63u) == 0u)
         P.wave_cost[wv] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     if (STAMPS) {
         __syncthreads();
@@ -1262,6 +1264,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
         SVO_FAIL(SVO_ERANGE, "svo_cast_rays: frame too large (2^26 wavefronts or more in one launch)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
+    P.n_waves = (uint32_t)(nthreads / 64);
     if ((d->flags & SVO_CAST_HORIZON_FIRST) && P.tile_rows_local <= kMaxOrderRows) {
         // shallowest centre ray first (a stable sort of the local rows by |dir.y| of their middle pixel)
         std::vector<std::pair<float, int32_t>> key(P.tile_rows_local);
