@@ -289,11 +289,6 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU; torch exchange)")
     ap.add_argument("--verify", action="store_true",
                     help="with an exchange: every rank checks the frames it displays against a one-GPU cast of them")
-    ap.add_argument("--order", default="none", choices=["none", "feedback", "sync"],
-                    help="dispatch order of the cast's waves: feedback = each launch records its waves' durations "
-                         "(svo_cast_desc.wave_cost) and svo_cast_order sorts them, longest first, on a side stream for the launch "
-                         "after next; sync = the same on the launch stream for the next launch; none = top tile rows first")
-    ap.add_argument("--order-group", type=int, default=16, help="svo_cast_order: waves per group kept together")
     ap.add_argument("--pipelined-steps", type=int, default=None,
                     help="N = 1: after the timed region, time this many more steps with consecutive launches on two "
                          "alternating streams (a launch's tail overlaps the next one's head), reported as `pipelined` "
@@ -381,7 +376,7 @@ def main():
         xmode = "torch" if (args.shade or args.exchange == "torch" or args.dist_backend != "nccl") else "capi"
     gdev = torch.device("cuda", dev)
     pipe_steps = args.steps if args.pipelined_steps is None else args.pipelined_steps
-    if gather or args.order != "none" or world > 1:
+    if gather or world > 1:
         pipe_steps = 0  # (an N = 1 measurement beside the contract's own)
     nbuf = 2 if (gather or pipe_steps) else 1  # the exchange (or the next launch) of step k overlaps step k+1
     outs = []
@@ -424,48 +419,12 @@ def main():
 
     xdone = [None] * nbuf
     cast_done = [torch.cuda.Event() for _ in range(nbuf)]
-    # cost-ordered dispatch: wave durations of launch k order launch k + 2 (feedback, sorted on a side
-    # stream while launch k + 1 runs) or launch k + 1 (sync)
-    nwaves = rt.Tree.blocks(desc)
-    ordering = args.order != "none"
-    ocost = [torch.zeros(nwaves, dtype=torch.int32, device=gdev) for _ in range(2)] if ordering else None
-    oorder = [torch.zeros(nwaves, dtype=torch.int32, device=gdev) for _ in range(2)] if ordering else None
-    ovalid = [False, False]
-    osort = [None, None]
-    ostream = torch.cuda.Stream(device=dev) if args.order == "feedback" else None
-
-    def set_order(k):
-        if not ordering:
-            return
-        j = k % 2 if args.order == "feedback" else 0
-        if osort[j] is not None:
-            stream.wait_event(osort[j])  # the sort that wrote this order (and read these costs) has passed
-        desc.wave_order = oorder[j].data_ptr() if ovalid[j] else None
-        desc.wave_cost = ocost[j].data_ptr()
-
-    def sort_order(k):
-        if not ordering:
-            return
-        if args.order == "feedback":
-            j = k % 2
-            e = torch.cuda.Event()
-            e.record(stream)
-            ostream.wait_event(e)
-            rt.Tree.cast_order(desc, ocost[j], oorder[j], ostream, group=args.order_group)
-            osort[j] = torch.cuda.Event()
-            osort[j].record(ostream)
-        else:
-            j = 0
-            rt.Tree.cast_order(desc, ocost[0], oorder[0], stream, group=args.order_group)
-        ovalid[j] = True
-
     def one_step(k, ev=None, pipe=False):
         b = k % nbuf
         stream = cstreams[k % 2] if pipe else cstreams[0]
         with torch.cuda.stream(stream):
             if xdone[b] is not None:
                 stream.wait_event(xdone[b])  # the exchange that read this buffer set has passed
-            set_order(k)
             if ev is not None:
                 ev[0].record(stream)
             if args.shade:
@@ -475,7 +434,6 @@ def main():
                 tree.cast(desc, outs[b], stream)
             if ev is not None:
                 ev[1].record(stream)
-            sort_order(k)
         if not gather:
             return
         if xmode == "capi":
@@ -614,10 +572,7 @@ def main():
                                                      "castRayFromCam semantics" % (cfg["origin"] + cfg["cam"] + (STEPS,)),
                    "ao_samples": args.ao, "shade": args.shade, "frames_per_step": nframes, "rays_per_step": W * H * nframes,
                    "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "gather": gather,
-                   "dispatch_order": {"none": "top tile rows first",
-                                      "feedback": "waves by the measured durations of the launch before last, longest first "
-                                                  "(svo_cast_order on a side stream)",
-                                      "sync": "waves by the previous launch's durations (svo_cast_order on the launch stream)"}[args.order],
+                   "dispatch_order": "top tile rows first",
                    "exchange": None if not gather else (
                        ("svo_exchange_frames (C ABI, RCCL send/recv group): 12-B wire records" + (" + AO counts" if args.ao else "") +
                         ", frame f to rank f %% N, unpacked on arrival, on a second stream overlapping the next cast")

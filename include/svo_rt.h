@@ -25,8 +25,8 @@ extern "C" {
 
 #define SVO_RT_VERSION 6  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
                              4: tree views (liquid stored for the shading pass), svo_shade_desc.scene / time;
-                             5: svo_cast_desc.wave_order / wave_cost + svo_cast_order (cost-ordered dispatch);
-                             6: svo_tree_save / svo_tree_load */
+                             6: svo_tree_save / svo_tree_load (5, a cost-ordered dispatch, was measured slower
+                             and removed) */
 
 enum {
     SVO_OK = 0,
@@ -216,14 +216,6 @@ typedef struct {
        of frame f follow those of frame f-1: svo_cast_count / svo_cast_blocks count all frames. */
     int32_t n_frames;
     const float* frame_origins;
-    /* frame mode, dispatch order (results identical): a frame launch is svo_cast_blocks(d) wavefronts,
-       one per pixel footprint ("wave" w = 0 .. blocks-1, in the default order: every frame's top tile
-       rows first).  wave_cost (device, optional): each wave writes its duration (100 MHz ticks) to
-       wave_cost[w].  wave_order (device, optional): launch block b casts wave wave_order[b], a
-       permutation of 0 .. blocks-1 — e.g. svo_cast_order of a previous launch's costs, longest first,
-       so the long waves of a frame start first and the launch does not end on them. */
-    const uint32_t* wave_order;
-    uint32_t* wave_cost;
 } svo_cast_desc;
 
 #define SVO_MAX_FRAMES 16
@@ -255,11 +247,6 @@ typedef struct {
 /* svo_cast_desc.flags (results identical): read nodes through 64-bit addresses even when the tree is
    small enough for 32-bit buffer offsets (trees of more than 2^28 nodes always use them) */
 #define SVO_CAST_WIDE_ADDR 2048
-
-/* wave_order from wave_cost (both svo_cast_blocks(d) entries, device): groups of `group` consecutive
-   waves (neighbouring footprints of a tile row) by descending cost of their longest wave (ties in any
-   order), the waves of a group kept together; one small kernel on hip_stream.  Frame descs only. */
-int svo_cast_order(const svo_cast_desc* d, const uint32_t* wave_cost, int32_t group, uint32_t* wave_order, void* hip_stream);
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

@@ -108,8 +108,6 @@ class CastDesc(C.Structure):
         ("stats", C.c_void_p),
         ("n_frames", C.c_int32),
         ("frame_origins", C.c_void_p),
-        ("wave_order", C.c_void_p),
-        ("wave_cost", C.c_void_p),
     ]
 
 
@@ -140,7 +138,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
-    "svo_cast_order", "svo_tree_save", "svo_tree_load",
+    "svo_tree_save", "svo_tree_load",
 )
 
 
@@ -176,7 +174,6 @@ def lib():
     # library builds of earlier revisions (tools/build_variant.py) loads them through this module)
     for name, at in (("svo_build_view", [vp, i32, C.POINTER(vp)]), ("svo_build_terrain_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
                      ("svo_build_terrain_gpu_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
-                     ("svo_cast_order", [C.POINTER(CastDesc), vp, i32, vp, vp]),
                      ("svo_tree_save", [vp, C.c_char_p]), ("svo_tree_load", [C.c_char_p, C.POINTER(vp)])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
@@ -537,14 +534,6 @@ class Tree:
         n = C.c_int64()
         _check(lib().svo_cast_blocks(C.byref(desc), C.byref(n)), "svo_cast_blocks")
         return n.value
-
-    @staticmethod
-    def cast_order(desc, wave_cost, wave_order, stream=None, group=1):
-        """wave_order (uint32 device tensor, svo_cast_blocks entries) = groups of `group` waves by
-        descending wave_cost (svo_cast_desc.wave_cost of a previous launch): longest first"""
-        s = getattr(stream, "cuda_stream", stream)
-        _check(lib().svo_cast_order(C.byref(desc), C.c_void_p(wave_cost.data_ptr()), group, C.c_void_p(wave_order.data_ptr()),
-                                    C.c_void_p(s) if s else None), "svo_cast_order")
 
     @staticmethod
     def alloc_hits(n, device, ao=False):

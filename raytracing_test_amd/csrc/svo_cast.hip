@@ -73,10 +73,6 @@ struct CastParams {
     float time;                 // deltaTime of the liquid wobble (low_res.frag:226)
     const Node* snodes;         // shading: the solid-view tree the shadow rays walk (nodes: the scene)
     const uint16_t* smats;
-    // frame mode dispatch order (svo_cast_desc.wave_order / wave_cost)
-    const uint32_t* wave_order;
-    uint32_t* wave_cost;
-    uint32_t n_waves;  // waves of the launch (a wave_order entry at or beyond it casts nothing)
     // shading: the highest stored voxel row of the scene / of the solid tree (tree_top_y); a ray
     // moving up above it that cannot wrap in y before its budget ends can hit nothing more
     int32_t top_scene, top_solid;
@@ -937,7 +933,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
     unsigned long long t_start = 0;
-    if ((STAMPS && threadIdx.x == 0) || P.wave_cost) t_start = __builtin_amdgcn_s_memrealtime();
+    if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     // per-lane node path (mask and first-child index of the interior node at each depth of the
     // last descent), [depth][lane]
     __shared__ uint64_t path_mask[(kMaxLevels - 1) * kBlock];
@@ -959,23 +955,19 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
-    uint32_t wv = 0u;
     if (P.mode == MODE_FRAME) {
         // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes.
         // The tile index is wave-uniform: its division runs on the scalar unit.
         // frames interleave wave by wave (every frame's long top rows first); the frame and tile
-        // indices are wave-uniform: their divisions run on the scalar unit.  A wave order (e.g. by
-        // the previous launch's costs) permutes the waves over the launch's blocks.
-        wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        if (P.wave_order) wv = __builtin_amdgcn_readfirstlane(P.wave_order[wv]);
-        if (wv >= P.n_waves) wv = P.n_waves;  // a malformed order: this block casts nothing (and records nothing)
+        // indices are wave-uniform: their divisions run on the scalar unit
+        const uint32_t wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
         const int32_t lane = (int32_t)(threadIdx.x & 63u);
         const uint32_t tq = tile / (uint32_t)P.tiles_x;
         int32_t trl = (int32_t)tq;
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
-        if (P.use_row_order) trl = tq < (uint32_t)kMaxOrderRows ? P.row_order[tq] : -1;
+        if (P.use_row_order) trl = P.row_order[tq];
         else if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
@@ -984,7 +976,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
         const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
         const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-        if (wv < P.n_waves && trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
             o[0] = P.frame_org[3 * fr + 0];
             o[1] = P.frame_org[3 * fr + 1];
@@ -1085,8 +1077,6 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
             P.ao[out] = (uint8_t)cnt;
         }
     }
-    if (P.wave_cost && P.mode == MODE_FRAME && wv < P.n_waves && (threadIdx.x & 63u) == 0u)
-        P.wave_cost[wv] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_start);
     if (STAMPS) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1231,7 +1221,6 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
         }
     }
     if (d->ray_dirs) {
-        if (d->wave_order || d->wave_cost) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: wave_order / wave_cost are for frame descs");
         P.mode = MODE_EXPLICIT;
         P.rdir = d->ray_dirs;
         P.rorg = d->ray_origins;
@@ -1240,8 +1229,6 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
         return SVO_OK;
     }
     P.mode = MODE_FRAME;
-    P.wave_order = d->wave_order;
-    P.wave_cost = d->wave_cost;
     raygen_init(P.rg, d->cam_dir, d->ppx, d->ppy, d->width, d->height);
     P.width = d->width;
     P.height = d->height;
@@ -1264,7 +1251,6 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
         SVO_FAIL(SVO_ERANGE, "svo_cast_rays: frame too large (2^26 wavefronts or more in one launch)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
-    P.n_waves = (uint32_t)(nthreads / 64);
     if ((d->flags & SVO_CAST_HORIZON_FIRST) && P.tile_rows_local <= kMaxOrderRows) {
         // shallowest centre ray first (a stable sort of the local rows by |dir.y| of their middle pixel)
         std::vector<std::pair<float, int32_t>> key(P.tile_rows_local);
@@ -1543,66 +1529,6 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
         const Material& m = t->palette[(info & HIT_BIT) ? (info & MAT_MASK) : 0u];
         *block = svo_block{m.flags, m.color, m.meta};
     }
-    return SVO_OK;
-}
-
-// ================================================================================================
-// cost-ordered dispatch (svo_cast_order): one workgroup counting-sorts the waves by descending cost
-// (4096 buckets of 16 ticks = 160 ns; longer costs share the top bucket), in LDS
-// ================================================================================================
-namespace {
-constexpr int kOrderThreads = 1024, kOrderBuckets = 4096;
-__global__ __launch_bounds__(kOrderThreads) void k_wave_order(const uint32_t* cost, uint32_t n, uint32_t group, uint32_t* order) {
-    __shared__ uint32_t hist[kOrderBuckets];
-    __shared__ uint32_t part[kOrderThreads];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t ng = (n + group - 1) / group;  // groups of `group` consecutive waves, keyed by their longest
-    for (uint32_t b = tid; b < kOrderBuckets; b += kOrderThreads) hist[b] = 0u;
-    __syncthreads();
-    auto key = [&](uint32_t g) {
-        uint32_t c = 0u;
-        for (uint32_t i = g * group; i < min(n, g * group + group); i++) c = max(c, cost[i]);
-        return (uint32_t)(kOrderBuckets - 1) - min(c >> 4, (uint32_t)(kOrderBuckets - 1));
-    };
-    for (uint32_t g = tid; g < ng; g += kOrderThreads) atomicAdd(&hist[key(g)], min(group, n - g * group));
-    __syncthreads();
-    // exclusive scan: 4 buckets per thread, then the threads' sums (Hillis-Steele over 1024)
-    constexpr uint32_t per = kOrderBuckets / kOrderThreads;
-    uint32_t loc[per], sum = 0u;
-    for (uint32_t k = 0; k < per; k++) {
-        loc[k] = sum;
-        sum += hist[tid * per + k];
-    }
-    part[tid] = sum;
-    __syncthreads();
-    for (uint32_t off = 1; off < kOrderThreads; off <<= 1) {
-        const uint32_t v = tid >= off ? part[tid - off] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    const uint32_t base = part[tid] - sum;
-    for (uint32_t k = 0; k < per; k++) hist[tid * per + k] = base + loc[k];
-    __syncthreads();
-    for (uint32_t g = tid; g < ng; g += kOrderThreads) {
-        const uint32_t m = min(group, n - g * group);
-        const uint32_t at = atomicAdd(&hist[key(g)], m);
-        for (uint32_t j = 0; j < m; j++) order[at + j] = g * group + j;
-    }
-}
-}  // namespace
-
-extern "C" int svo_cast_order(const svo_cast_desc* d, const uint32_t* wave_cost, int32_t group, uint32_t* wave_order, void* stream) {
-    if (!d || !wave_cost || !wave_order) SVO_FAIL(SVO_EINVAL, "svo_cast_order: NULL argument");
-    if (group < 1) SVO_FAIL(SVO_EINVAL, "svo_cast_order: group must be >= 1");
-    if (d->ray_dirs) SVO_FAIL(SVO_EINVAL, "svo_cast_order: frame descs only");
-    int64_t n = 0;
-    int rc = svo_cast_blocks(d, &n);
-    if (rc) return rc;
-    if (n == 0) return SVO_OK;
-    if (n > (int64_t)1 << 26) SVO_FAIL(SVO_ERANGE, "svo_cast_order: too many waves");
-    hipLaunchKernelGGL(k_wave_order, dim3(1), dim3(kOrderThreads), 0, (hipStream_t)stream, wave_cost, (uint32_t)n, (uint32_t)group, wave_order);
-    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
 

@@ -439,50 +439,6 @@ def test_depth14_4k_sampled_parity(rt, oracle_mod, torch_cuda):
     del t
 
 
-def test_wave_order_and_cost(rt, gtree, torch_cuda):
-    """cost-ordered dispatch (svo_cast_desc.wave_order / wave_cost, svo_cast_order): any permutation of
-    the waves gives the same records; the recorded costs sort into a permutation, longest first"""
-    torch = torch_cuda
-    org, cam = (4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0))
-    for W, H, nf in ((240, 136, 1), (100, 37, 3)):
-        origins = [(4.0 + 16 * f, 90.0, 4.0) for f in range(nf)]
-        d = rt.Tree.frame_desc(origins[0], cam, W, H, 300, frame_origins=origins if nf > 1 else None)
-        n, nw = rt.Tree.count(d), rt.Tree.blocks(d)
-        base = rt.Tree.alloc_hits(n, 0)
-        gtree.cast(d, base)
-        cost = torch.zeros(nw, dtype=torch.int32, device="cuda")
-        d.wave_cost = cost.data_ptr()
-        out = rt.Tree.alloc_hits(n, 0)
-        gtree.cast(d, out)
-        order = torch.full((nw,), -1, dtype=torch.int32, device="cuda")
-        rt.Tree.cast_order(d, cost, order)
-        torch.cuda.synchronize()
-        c, o = cost.cpu().numpy().view(np.uint32), order.cpu().numpy()
-        assert (c > 0).all()
-        assert np.array_equal(np.sort(o), np.arange(nw))  # a permutation
-        key = np.minimum(c[o] >> 4, 4095)
-        assert np.all(np.diff(key.astype(np.int64)) <= 0)  # longest first
-        for g in (3, 16):  # groups of consecutive waves keyed by their longest, kept together
-            og = torch.full((nw,), -1, dtype=torch.int32, device="cuda")
-            rt.Tree.cast_order(d, cost, og, group=g)
-            torch.cuda.synchronize()
-            q = og.cpu().numpy()
-            assert np.array_equal(np.sort(q), np.arange(nw))
-            starts = q[np.concatenate([[True], np.diff(q) != 1])]
-            assert np.all(starts % g == 0)
-            gk = np.array([np.minimum(c[s:s + g].max() >> 4, 4095) for s in starts], np.int64)
-            assert np.all(np.diff(gk) <= 0)
-        for perm in (o, np.random.default_rng(nf).permutation(nw).astype(np.int32)):
-            po = torch.from_numpy(np.ascontiguousarray(perm)).cuda()
-            d.wave_order = po.data_ptr()
-            gtree.cast(d, out)
-            torch.cuda.synchronize()
-            for k in base:
-                assert torch.equal(out[k], base[k]), k
-        d.wave_order = None
-        d.wave_cost = None
-
-
 def test_exchange_single_rank_python(rt, gtree, torch_cuda):
     """svo_exchange_frames through the Python binding (rt.Exchange) on a one-rank RCCL communicator: the
     frames it unpacks equal the cast records (ragged frame, several frames per launch, AO counts)"""
