@@ -282,6 +282,7 @@ def main():
                     help="capi: svo_exchange_frames (RCCL inside libsvo_rt); torch: all_to_all_single of wire records")
     ap.add_argument("--force-exchange", action="store_true", help="run the exchange at N=1 too (a one-rank RCCL communicator)")
     ap.add_argument("--cols", type=int, default=None)
+    ap.add_argument("--origin", default=None, help="camera position x,y,z (default: the config's; e.g. a non-integral one)")
     ap.add_argument("--iterative", action="store_true", help="A/B: voxel-by-voxel DDA (SVO_CAST_ITERATIVE)")
     ap.add_argument("--stats", action="store_true", help="print traversal counters of one extra frame to stderr")
     ap.add_argument("--cast-flags", type=int, default=0, help="extra SVO_CAST_* bits (experiments)")
@@ -317,6 +318,8 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.cols is not None:
         cfg["cols"] = args.cols
+    if args.origin is not None:
+        cfg["origin"] = tuple(float(v) for v in args.origin.split(","))
     W, H, STEPS = cfg["W"], cfg["H"], cfg["steps"]
     if args.shade and args.ao:
         ap.error("--shade and --ao are separate workloads")

@@ -247,6 +247,12 @@ typedef struct {
 /* svo_cast_desc.flags (results identical): read nodes through 64-bit addresses even when the tree is
    small enough for 32-bit buffer offsets (trees of more than 2^28 nodes always use them) */
 #define SVO_CAST_WIDE_ADDR 2048
+/* svo_cast_desc.flags (results identical): the kernel instance picks itself by the origins — from
+   integral origins every ray's crossings are exact linear sums; other rays cross empty regions in
+   exact segments.  SEGMENTS forces the segment-capable instance, LINEAR_ONLY the other (where rays
+   that are not linear then step voxel by voxel) */
+#define SVO_CAST_SEGMENTS 4096
+#define SVO_CAST_LINEAR_ONLY 8192
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

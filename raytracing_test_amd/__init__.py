@@ -41,6 +41,8 @@ CAST_TILE_8X8 = 256  # scheduling: one wavefront per 8x8 tile (default: 16x4 pix
 CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel tile row
 CAST_HORIZON_FIRST = 1024  # scheduling: tile rows with the shallowest centre ray first
 CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (results identical)
+CAST_SEGMENTS = 4096  # force the kernel instance with segment-exact crossings (results identical)
+CAST_LINEAR_ONLY = 8192  # force the instance without them: non-linear rays step voxel by voxel (results identical)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
@@ -580,6 +582,20 @@ class Tree:
         if sync:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return out
+
+    def cast_stats(self, origin, cam_dir, width, height, steps, flags=0):
+        """Traversal counters of one frame (SVO_CAST_STATS), per ray: {STAT_NAMES[k]: value}."""
+        torch = _torch()
+        d = self.frame_desc(origin, cam_dir, width, height, steps, None, None, 0, 1, flags | CAST_STATS, 0, 5)
+        n = self.count(d)
+        dev = self.info().device
+        st = torch.zeros(STATS_HEADER + 2 * self.blocks(d) + n, dtype=torch.int64, device=torch.device("cuda", dev))
+        d.stats = st.data_ptr()
+        out = self.alloc_hits(n, dev)
+        self.cast(d, out)
+        _check(lib().svo_sync(None), "svo_sync")
+        v = st[:len(STAT_NAMES)].cpu().numpy().astype(np.float64)
+        return {k: v[i] / max(1.0, v[0]) for i, k in enumerate(STAT_NAMES)}
 
     def cast_rays(self, dirs, origins=None, steps=300, origin=(0.0, 0.0, 0.0), out=None, stream=None, sync=True, flags=0):
         """Explicit rays: dirs / origins are (n, 3) float32 device tensors."""

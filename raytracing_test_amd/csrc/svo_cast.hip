@@ -91,14 +91,22 @@ struct Hit {
 // Exact closed-form skipping.  castRayFromCam's axis choice (ray_caster.cpp:71-80) is, for non-NaN
 // values, the lexicographic minimum of (T_axis, rank) with rank z < y < x: x wins only when
 // strictly smallest, y beats z only when strictly smaller.  Each axis' crossings form the sequence
-// T, T+a, T+2a, ... (deltaPos += absDelta).  absDelta is an f32 reciprocal widened to f64, so it
-// carries 24 significant bits; when every partial sum a ray can reach (<= budget+2 terms) stays
-// below 2^(lsb+53) — lsb = lowest set bit of T and a — every sum is exact and T + k*a computed
-// directly equals the k-fold accumulation bit for bit.  Such a ray ("fast") crosses an empty
-// region in O(1): the first event to leave the region is the lexicographic minimum of the three
-// per-axis exit events, and the events before it on the other axes are counted by division
-// (with an exact fix-up).  Rays that fail the test step voxel by voxel (still without memory
-// traffic inside known-empty regions).  Both paths give identical results (tests).
+// T, fl(T+a), fl(fl(T+a)+a), ... (deltaPos += absDelta in double).  absDelta is an f32 value
+// widened to f64: 24 significant bits, a multiple of 2^(ea-23).
+//  * Linear rays: when every partial sum a ray can reach (<= budget+2 terms) stays below
+//    2^(lsb+53) — lsb = lowest set bit of T and a — every sum is exact and T + k*a computed directly
+//    equals the k-fold accumulation bit for bit (e.g. always from integral camera positions).
+//  * Every other ray (budget < 2^20, finite values): |T| stays below 2^(ea+22), so a is a multiple
+//    of ulp(T) and every crossing below B = 2^(e+1) (e = the binade of |T|) is an exact,
+//    representable multiple of ulp(T); the first crossing at or above B is that exact sum rounded
+//    once, which fma(k, a, T) also computes.  Only later crossings (one more rounding per binade
+//    entered) drift from the closed form, so the crossings are exact segment by segment
+//    (seg_cap), and an empty region is crossed in a few moves (skip_box<true>).
+// A ray crosses an empty region in O(1): the first event to leave the region is the lexicographic
+// minimum of the three per-axis exit events, and the events before it on the other axes are
+// counted by division (with an exact fix-up).  Rays outside both domains step voxel by voxel
+// (still without memory traffic inside known-empty regions).  All paths give identical results
+// (tests).
 // ------------------------------------------------------------------------------------------------
 // lowest set bit (power of two) of |x|: x finite and nonzero; denormals -> 1 << 20 ("not fast")
 __device__ __forceinline__ int dbl_lsb(uint32_t hi, uint32_t lo) {
@@ -108,12 +116,18 @@ __device__ __forceinline__ int dbl_lsb(uint32_t hi, uint32_t lo) {
     return e == 0 ? (1 << 20) : e - 1075 + tz;
 }
 
+// a: positive, normal, finite; T: finite (the closed forms' domain)
+__device__ __forceinline__ bool axis_ok(double T, double a) {
+    const uint32_t th = (uint32_t)((uint64_t)__double_as_longlong(T) >> 32) & 0x7FFFFFFFu;
+    const uint32_t ah = (uint32_t)((uint64_t)__double_as_longlong(a) >> 32);
+    const uint32_t et = th >> 20, ea = (ah >> 20) & 0x7FFu;
+    return !(ah >> 31) && ea != 0u && ea != 0x7FFu && et != 0x7FFu;
+}
+
+// every partial sum exact ("linear" axis: no rounding at all); axis_ok(T, a) holds
 __device__ __forceinline__ bool exact_axis(double T, double a, int32_t budget) {
     const uint32_t th = (uint32_t)((uint64_t)__double_as_longlong(T) >> 32) & 0x7FFFFFFFu, tl = (uint32_t)__double_as_longlong(T);
     const uint32_t ah = (uint32_t)((uint64_t)__double_as_longlong(a) >> 32), al = (uint32_t)__double_as_longlong(a);
-    const uint32_t et = th >> 20, ea = (ah >> 20) & 0x7FFu;
-    // a: positive, normal, finite; T: finite (zero allowed: no constraint from it)
-    if ((ah >> 31) || ea == 0u || ea == 0x7FFu || et == 0x7FFu) return false;
     const int u = (th | tl) ? min(dbl_lsb(th, tl), dbl_lsb(ah, al)) : dbl_lsb(ah, al);
     const double bound = __builtin_fabs(T) + (double)(budget + 2) * a;
     const int eb = (int)((uint32_t)((uint64_t)__double_as_longlong(bound) >> 52) & 0x7FFu) - 1023;
@@ -287,17 +301,59 @@ __device__ __forceinline__ int32_t count_est(double T, double a, float inva, dou
     return (int32_t)mu;
 }
 
-// Cross an empty box in one move, branch-free over the exit axis: e[k] = steps along axis k that
-// leave the box.  Returns false (state unchanged) when the budget ends inside the box.
-__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3]) {
-    // ex = steps to leave, less one; exits beyond the budget are clamped (safe: total > steps)
+// Exact segments.  From any state (T, a), the crossings T + i*a are multiples of 2^v, v = the lower
+// of the lowest set bits of T and a, so every crossing below B = 2^(v+53) is exact and representable,
+// and the first one at or above B is that sum rounded once, as fma(i, a, T) computes it too.  B is at
+// least 2^(e+1) (e = the binade of |T|: T is a multiple of ulp(T), and a of 2^(ea-23) > ulp(T) as
+// |T| < 2^(ea+22)); for a ray from a non-integral origin it is typically hundreds of crossings away,
+// and past it each binade the crossings enter costs one rounding.  seg_cap returns an index of a
+// crossing below B (at most the last one): the crossings 0 .. seg_cap + 1 are fma-exact.
+// lowest set bit exponent of |T| (zero: none, 2^20; subnormal: -1074, a safe underestimate)
+__device__ __forceinline__ int32_t lsb_exp(double T) {
+    const uint64_t b = (uint64_t)__double_as_longlong(T);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    const int32_t e = (int32_t)((hi >> 20) & 0x7FFu);
+    const int32_t tz = lo ? (int32_t)__builtin_ctz(lo) : 32 + (int32_t)__builtin_ctz((hi & 0xFFFFFu) | 0x100000u);
+    return e != 0 ? e - 1075 + tz : ((b << 1) == 0ull ? (1 << 20) : -1074);
+}
+// A ray is linear, by a cheap sufficient test on its origin, when every coordinate is integral or
+// half-integral: dda_axis then starts at T = a, 0, a/2, 3a/2 or -a/2 (a multiple of half of a's
+// lowest set bit, 2^(la-1)), and with a budget below 2^20 every sum stays below 2^(la-1+53) — the
+// camera positions of integral poses, and the cell centres shadow and AO rays start from.
+__device__ __forceinline__ bool lin_origin(float o) {
+    const float o2 = o + o;
+    return o2 == __builtin_truncf(o2) && __builtin_fabsf(o) < 1073741824.0f;
+}
+
+// x = (B - T)/a is estimated as x~ within 2^-22 relative (f32 roundings, the 1-ulp reciprocal), so
+// floor(x~ * (1 - 2^-20)) < x: at most the count of crossings below B, less one (almost always equal)
+__device__ __forceinline__ int32_t seg_cap(double T, float af, float inva) {
+    const uint32_t ab = __float_as_uint(af);
+    const int32_t la = (int32_t)((ab >> 23) & 0xFFu) - 150 + (int32_t)__builtin_ctz(ab | 0x800000u);  // a: normal
+    const int32_t be = min(max(min(lsb_exp(T), la) + 53 + 1023, 1), 0x7FF);  // biased exponent of B (0x7FF: inf)
+    const double B = __longlong_as_double((long long)((uint64_t)(uint32_t)(be << 20) << 32));
+    uint32_t c;
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(c) : "v"((float)(B - T) * inva * 0.99999905f));  // saturates (inf: 2^32 - 1)
+    return (int32_t)min(c, 1u << 30);  // (never negative: every skip takes at least its exit step)
+}
+
+// Cross an empty box, branch-free over the exit axis: ex[k] = steps along axis k that leave the box,
+// less one.  Returns false (state unchanged) when the budget ends inside the box.  seg (wave-uniform:
+// the wave holds rays that are not linear): each axis' exit event is also held to its exact segment (seg_cap); an exit on such a
+// bound is a virtual one inside the box (the next lookup finds the same empty cell in the parent's
+// mask, without a load, and the crossing continues).
+__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) {
+    // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) e[k] = min(ex[k], R.steps);
+    if (seg) {  // wave-uniform
+#pragma unroll
+        for (int k = 0; k < 3; k++) e[k] = min(e[k], seg_cap(R.T[k], R.af[k], R.inv_a(k)));
+    }
     double E[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        e[k] = min(ex[k], R.steps);
-        E[k] = on_grid(R.T[k], e[k], R.a(k));
-    }
+    for (int k = 0; k < 3; k++) E[k] = on_grid(R.T[k], e[k], R.a(k));
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     // exit flags as lane masks (SGPRs): selects and tie terms read them directly
     const uint64_t mx = __ballot((E[0] < E[1]) && (E[0] < E[2]));
@@ -566,7 +622,7 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // ESCAPE (shading rays whose end position is not output): a ray moving up above the highest stored
 // voxel row `top` (wrapped) whose budget cannot carry it past the extent in y leaves the loop as a
 // miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off).
-template <bool STATS, bool REFLECT = false, bool ESCAPE = false, class Mem>
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1) {
@@ -583,9 +639,19 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    // budget < 2^20 also keeps the f32 count estimates within 1/4 of the truth (count_est)
-    bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) &&
-                exact_axis(R.T[2], R.a(2), budget);
+    // closed-form crossings (fast): budget < 2^20 also keeps the f32 count estimates within 1/4 of
+    // the truth (count_est, seg_cap); linear rays need no segment bounds, and a wave of linear rays
+    // takes the cheaper crossing
+    bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
+                axis_ok(R.T[2], R.a(2));
+    // SEG: the instance carries segment-bounded crossings (the host picks it when rays can be
+    // non-linear: need_seg).  The other one takes closed-form crossings only for rays that are
+    // linear by a cheap sufficient test (lin_origin) and steps any other ray voxel by voxel: the same
+    // results either way, and the linear waves keep the shorter code.
+    bool lin = SEG ? fast && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) && exact_axis(R.T[2], R.a(2), budget)
+                   : fast && lin_origin(o[0]) && lin_origin(o[1]) && lin_origin(o[2]);
+    if (!SEG) fast = lin;
+    const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
     uint32_t ud[3];
     dir_flags(R.s, ud);
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
@@ -632,7 +698,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
                        box_exits(w, R.s, sh, par.mask, ud, ex);
-                       return skip_box(R, ex);
+                       return skip_box(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                    }())) {
             if (STATS && fast) st.skip_out++;
             if (fast) {
@@ -737,8 +803,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                     R.af[k] = (float)ad;
                     R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
                 }
-                fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && exact_axis(R.T[0], R.a(0), R.steps) &&
-                       exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
+                fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
+                       axis_ok(R.T[2], R.a(2));
+                lin = fast && exact_axis(R.T[0], R.a(0), R.steps) && exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
+                if (!SEG) fast = lin;  // (REFLECT runs in SEG instances)
             }
             dda_step(R);
             done = false;
@@ -813,6 +881,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (hit ? mat & MAT_MASK : 0u);
     return h;
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // Shading: low_res.frag's colour model over castRayFromCam hits — sky
@@ -923,7 +992,7 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem
 }
 
 // WIDE: 64-bit node addresses (trees above kNarrowNodes nodes, or SVO_CAST_WIDE_ADDR)
-template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE>
+template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
@@ -1008,7 +1077,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<false, true, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene);
+        const Hit h = trace<false, true, true, SEG>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -1048,7 +1117,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS, false, false, SEG>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
@@ -1187,10 +1256,30 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
 // buffer offset reaches (or on request)
 bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap > kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
 
+// seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always)
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
-void launch_cast(bool wide, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
-    if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true>), grid, block, 0, st, P);
-    else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false>), grid, block, 0, st, P);
+void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
+    if (SHADE || seg) {
+        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, 0, st, P);
+        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false, true>), grid, block, 0, st, P);
+    } else {
+        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, true, false>), grid, block, 0, st, P);
+        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, false, false>), grid, block, 0, st, P);
+    }
+}
+
+// Can the launch hold rays that are not linear (svo_cast.hip, "Exact closed-form skipping")?  From an
+// integral or half-integral origin every ray is (lin_origin); explicit rays are not inspected.
+// Either instance gives the same results: this only picks the faster one.
+static bool need_seg(const CastParams& P) {
+    if (P.flags & (SVO_CAST_ITERATIVE | SVO_CAST_LINEAR_ONLY)) return false;
+    if (P.flags & SVO_CAST_SEGMENTS) return true;
+    if (P.mode == MODE_EXPLICIT) return true;
+    const int32_t nf = P.mode == MODE_FRAME ? P.n_frames : 1;
+    const float* org = P.mode == MODE_FRAME ? P.frame_org : P.org;
+    for (int32_t i = 0; i < 3 * nf; i++)
+        if (!(2.0f * org[i] == __builtin_truncf(2.0f * org[i]) && __builtin_fabsf(org[i]) < 1073741824.0f)) return true;
+    return false;
 }
 
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
@@ -1440,7 +1529,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
-    launch_cast<false, false, false, true>(wide_nodes(t, d->flags) || wide_nodes(sc, d->flags), dim3((uint32_t)blocks), dim3(kBlock),
+    launch_cast<false, false, false, true>(wide_nodes(t, d->flags) || wide_nodes(sc, d->flags), true, dim3((uint32_t)blocks), dim3(kBlock),
                                            (hipStream_t)stream, P);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
@@ -1471,16 +1560,16 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_cast_rays: too many rays for one launch");
     const dim3 grid((uint32_t)blocks), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
-    const bool wide = wide_nodes(t, d->flags);
+    const bool wide = wide_nodes(t, d->flags), seg = need_seg(P);
     if (P.ao_n > 0) {
-        if (P.flags & SVO_CAST_STATS) launch_cast<true, true, true, false>(wide, grid, block, st, P);
-        else launch_cast<false, false, true, false>(wide, grid, block, st, P);
+        if (P.flags & SVO_CAST_STATS) launch_cast<true, true, true, false>(wide, seg, grid, block, st, P);
+        else launch_cast<false, false, true, false>(wide, seg, grid, block, st, P);
     } else if (P.flags & SVO_CAST_STATS) {
-        launch_cast<true, true, false, false>(wide, grid, block, st, P);
+        launch_cast<true, true, false, false>(wide, seg, grid, block, st, P);
     } else if (P.flags & SVO_CAST_TIMELINE) {
-        launch_cast<false, true, false, false>(wide, grid, block, st, P);
+        launch_cast<false, true, false, false>(wide, seg, grid, block, st, P);
     } else {
-        launch_cast<false, false, false, false>(wide, grid, block, st, P);
+        launch_cast<false, false, false, false>(wide, seg, grid, block, st, P);
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
@@ -1513,7 +1602,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
     P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    launch_cast<false, false, false, false>(wide_nodes(t, 0), dim3(1), dim3(kBlock), nullptr, P);
+    launch_cast<false, false, false, false>(wide_nodes(t, 0), need_seg(P), dim3(1), dim3(kBlock), nullptr, P);
     unsigned char host[64];
     hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
     if (e != hipSuccess) SVO_FAIL(SVO_EDEVICE, std::string("svo_cast_ray_from_cam: ") + hipGetErrorString(e));

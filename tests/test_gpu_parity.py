@@ -66,7 +66,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
     for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST,
-                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR):
+                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_LINEAR_ONLY):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -132,7 +132,7 @@ def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
     dirs = np.array([c[1] for c in cases], np.float32)
     for steps in sorted(set(c[2] for c in cases)):
         sel = [i for i, c in enumerate(cases) if c[2] == steps]
-        for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR):
+        for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR, rt.CAST_LINEAR_ONLY):
             out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps, flags)
             compare(rt, gtree, out, ref, "edge S=%d flags=%d" % (steps, flags))
 
@@ -166,7 +166,7 @@ def test_random_rays(rt, torch_cuda, gtree, ref_world_oracle):
     # octant box [-256, 0)^3 for these origins
     keep = ~_segment_hits_box(org, d, 301.0, np.full(3, -256.0), np.zeros(3))
     org, d = org[keep], d[keep]
-    for flags in (0, rt.CAST_ITERATIVE):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY):
         out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, org, d, 300, flags)
         compare(rt, gtree, out, ref, "random flags=%d" % flags)
 
@@ -355,6 +355,32 @@ def test_depth12_budget_ends_in_air(rt, oracle_mod, depth12, pose, steps):
     assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
     assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
     assert (~sub["hit"]).mean() > 0.2  # most of these rays end their budget in the air
+
+
+@pytest.mark.parametrize("org", [(4.37, 90.61, 4.23), (-7.3, 88.125, 1000.01)])
+def test_depth12_fractional_camera(rt, oracle_mod, depth12, org):
+    """C3 from non-integral camera positions, S = 16384: the rays are not linear (their crossings
+    round once per binade), so the kernel crosses empty regions in exact segments (svo_cast.hip,
+    seg_cap).  Sampled pixels (top and bottom rows, the horizon band) against the oracle; the whole
+    frame identical to the voxel-by-voxel path; still O(1) crossings (not voxel stepping)."""
+    T = oracle_mod.Tree.terrain(6, 4096, 4096)
+    dn = rt.normalize([1, -0.45, 1])
+    W, H = 1920, 1080
+    out = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384))
+    rng = np.random.default_rng(int(abs(org[0]) * 100))
+    pix = np.unique(np.concatenate([rng.integers(0, W * H, 4000), np.arange(W * 539, W * 540), np.arange(0, W, 3), np.arange(W * (H - 1), W * H, 3)]))
+    ref = T.cast_frame(org, dn, W, H, 16384, pixels=pix, nthreads=16)
+    assert ref["rc"] == 0
+    sub = {k: v[pix] for k, v in out.items()}
+    assert np.array_equal(sub["pos"], ref["pos"]) and np.array_equal(sub["steps"], ref["steps"])
+    assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
+    assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
+    for flags in (rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY):
+        o2 = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384, flags=flags))
+        for k in out:
+            assert np.array_equal(out[k], o2[k]), (k, flags)
+    st = depth12.cast_stats(org, dn, W, H, 16384)
+    assert st["skips"] > 5.0 and st["lookups"] < 3.0 * st["skips"], st  # empty space crossed in O(1) moves
 
 
 def test_depth12_full_frame_properties(rt, depth12):
