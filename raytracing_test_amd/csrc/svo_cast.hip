@@ -73,7 +73,7 @@ struct CastParams {
     float time;                 // deltaTime of the liquid wobble (low_res.frag:226)
     const Node* snodes;         // shading: the solid-view tree the shadow rays walk (nodes: the scene)
     const uint16_t* smats;
-    // shading: the highest stored voxel row of the scene / of the solid tree (tree_top_y); a ray
+    // the highest stored voxel row of the scene / of the solid tree (tree_top_y; casts: top_solid); a ray
     // moving up above it that cannot wrap in y before its budget ends can hit nothing more
     int32_t top_scene, top_solid;
 };
@@ -625,7 +625,7 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
-                                     Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1) {
+                                     Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1) {
     Ray R;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -666,6 +666,17 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     par.sh = 2u * (uint32_t)P.levels;
     bool done = R.steps <= 0;
     if (!done) dda_step(R);
+    // pre_top (>= 0: the tree's highest stored voxel row, tree_top_y): a ray starting above it is in
+    // one empty region {y > pre_top} (every x, z; up to the wrap in y) and crosses it in one move,
+    // exactly like a box (false: its budget ends up there, state unchanged, the loop walks it)
+    if (pre_top >= 0 && fast && !done) {
+        uint32_t w[3];
+        wrap3(R, wm, w);
+        if ((int32_t)w[1] > pre_top) {
+            const int32_t ex[3] = {R.steps, R.s[1] < 0 ? (int32_t)w[1] - pre_top - 1 : (int32_t)(wm - w[1]), R.steps};
+            skip_box(R, ex, wseg);
+        }
+    }
     // one back-edge: every path through the body ends at the loop latch
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
@@ -1077,7 +1088,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<false, true, true, SEG>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene);
+        const Hit h = trace<false, true, true, SEG>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -1118,7 +1129,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     } else if (out >= 0) {
         Parent pfin;
         const Hit h = trace<STATS, false, false, SEG>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
-                                   nullptr, AO ? &pfin : nullptr);
+                                   nullptr, AO ? &pfin : nullptr, -1, P.top_solid);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -1290,6 +1301,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.mat_flags = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t->d_pal) + t->dev_pal_n * 8);
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
+    P.top_solid = t->dev_top_y;  // the empty region above the tree's highest voxel row (trace: pre_top)
     P.steps = d->steps;
     P.flags = d->flags;
     P.stats = reinterpret_cast<unsigned long long*>(d->stats);
@@ -1429,6 +1441,7 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     t->dev_node_cap = ncap;
     t->dev_mat_cap = mcap;
     t->synced_nodes = t->nodes.size();
+    t->dev_top_y = tree_top_y(t);
     t->synced_mats = t->mats.size();
     t->dirty_nodes.clear();
     t->full_upload = false;
@@ -1450,6 +1463,7 @@ int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_
     t->dev_node_cap = node_cap;
     t->dev_mat_cap = mat_cap;
     t->synced_nodes = t->nodes.size();
+    t->dev_top_y = tree_top_y(t);
     t->synced_mats = t->mats.size();
     t->dirty_nodes.clear();
     t->full_upload = false;
@@ -1484,6 +1498,7 @@ extern "C" int svo_tree_sync(svo_tree* t) {
     }
     t->dirty_nodes.clear();
     t->synced_nodes = t->nodes.size();
+    t->dev_top_y = tree_top_y(t);
     t->synced_mats = t->mats.size();
     return SVO_OK;
 }
@@ -1516,8 +1531,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     P.snodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.smats = reinterpret_cast<const uint16_t*>(t->d_mats);
     P.time = sd->time;
-    P.top_scene = tree_top_y(sc);
-    P.top_solid = tree_top_y(t);
+    P.top_scene = sc->dev_top_y;
+    P.top_solid = t->dev_top_y;
     P.rgba = reinterpret_cast<float4*>(rgba);
     for (int k = 0; k < 3; k++) {
         P.sun[k] = sd->sun_dir[k];
@@ -1594,6 +1609,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.mode = MODE_SINGLE;
+    P.top_solid = t->dev_top_y;
     P.steps = steps;
     for (int a = 0; a < 3; a++) {
         P.org[a] = pos[a];

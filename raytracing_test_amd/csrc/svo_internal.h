@@ -68,6 +68,8 @@ struct svo_tree {
     // highest voxel row holding a stored voxel (tree_top_y; -1: empty tree), cached until an edit
     mutable int32_t top_y = -1;
     mutable bool top_valid = false;
+    mutable std::mutex top_mu;  // (casts from several threads compute it once)
+    int32_t dev_top_y = -1;     // tree_top_y of the image in HBM (set by upload / adopt / sync; -1: none)
 };
 
 namespace svo {

@@ -1007,6 +1007,7 @@ int32_t top_y_of(const svo_tree* t, uint32_t ni, int32_t y0, int depth, int32_t 
 }  // namespace
 
 int32_t svo::tree_top_y(const svo_tree* t) {
+    std::lock_guard<std::mutex> lock(t->top_mu);
     if (!t->top_valid) {
         t->top_y = t->nodes.empty() ? -1 : top_y_of(t, 0, 0, 0, -1);
         t->top_valid = true;
