@@ -121,7 +121,7 @@ __device__ __forceinline__ bool axis_ok(double T, double a) {
     const uint32_t th = (uint32_t)((uint64_t)__double_as_longlong(T) >> 32) & 0x7FFFFFFFu;
     const uint32_t ah = (uint32_t)((uint64_t)__double_as_longlong(a) >> 32);
     const uint32_t et = th >> 20, ea = (ah >> 20) & 0x7FFu;
-    return !(ah >> 31) && ea != 0u && ea != 0x7FFu && et != 0x7FFu;
+    return ((unsigned)((ah >> 31) == 0u) & (unsigned)(ea - 1u < 0x7FEu) & (unsigned)(et != 0x7FFu)) != 0u;  // (branch-free)
 }
 
 // every partial sum exact ("linear" axis: no rounding at all); axis_ok(T, a) holds
@@ -642,14 +642,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // closed-form crossings (fast): budget < 2^20 also keeps the f32 count estimates within 1/4 of
     // the truth (count_est, seg_cap); linear rays need no segment bounds, and a wave of linear rays
     // takes the cheaper crossing
-    bool fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 20) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
-                axis_ok(R.T[2], R.a(2));
+    // (bitwise ands: one straight-line computation, no branch per term)
+    bool fast = ((unsigned)!(P.flags & SVO_CAST_ITERATIVE) & (unsigned)(budget < (1 << 20)) & (unsigned)axis_ok(R.T[0], R.a(0)) &
+                 (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2))) != 0u;
     // SEG: the instance carries segment-bounded crossings (the host picks it when rays can be
     // non-linear: need_seg).  The other one takes closed-form crossings only for rays that are
     // linear by a cheap sufficient test (lin_origin) and steps any other ray voxel by voxel: the same
     // results either way, and the linear waves keep the shorter code.
     bool lin = SEG ? fast && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) && exact_axis(R.T[2], R.a(2), budget)
-                   : fast && lin_origin(o[0]) && lin_origin(o[1]) && lin_origin(o[2]);
+                   : ((unsigned)fast & (unsigned)lin_origin(o[0]) & (unsigned)lin_origin(o[1]) & (unsigned)lin_origin(o[2])) != 0u;
     if (!SEG) fast = lin;
     const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
     uint32_t ud[3];

@@ -71,7 +71,9 @@ constexpr uint32_t kNoHit = 0xFFFFFFFFu;  // trace: material id while no voxel w
 // ------------------------------------------------------------------------------------------------
 SVO_HD float div_rn(float a, float b) { return (float)((double)a / (double)b); }
 #if defined(__HIP_DEVICE_COMPILE__)
-SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
+// HIP's f32 square root is correctly rounded (v_sqrt_f32 and an FMA residual check of the two
+// neighbouring floats), so it equals the double square root rounded once, at f32 cost
+SVO_HD float sqrt_rn(float a) { return __builtin_sqrtf(a); }
 #else
 SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
 #endif
