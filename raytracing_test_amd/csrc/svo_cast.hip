@@ -807,7 +807,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 for (int k = 0; k < 3; k++) {
                     const float dk = bounce->d[k];
                     const int32_t s = dk < 0.0f ? -1 : 1;
-                    const double delta = (double)svo::div_rn(1.0f, dk);
+                    const double delta = (double)svo::rcp_rn(dk);
                     const double ad = delta >= 0.0 ? delta : -delta;
                     if (s < 0) ex[k] -= 1.0;
                     R.T[k] = ad - (ex[k] - (double)R.r[k]) * delta;

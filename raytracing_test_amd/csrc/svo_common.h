@@ -78,6 +78,22 @@ SVO_HD float sqrt_rn(float a) { return __builtin_sqrtf(a); }
 SVO_HD float sqrt_rn(float a) { return (float)__builtin_sqrt((double)a); }
 #endif
 
+// 1/x correctly rounded.  Device: for |x| in [2^-126, 2^126) (x and 1/x normal), v_rcp_f32 and
+// one FMA Newton step give exactly div_rn(1, x) — checked for every such float, both signs
+// (tools/micro/rcp_check.hip); other x (zero, subnormal, huge, inf, NaN) take the division.
+#if defined(__HIP_DEVICE_COMPILE__)
+SVO_HD float rcp_rn(float x) {
+    const float ax = __builtin_fabsf(x);
+    if (ax >= 0x1p-126f && ax < 0x1p126f) {
+        const float r0 = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r0, 1.0f), r0, r0);
+    }
+    return div_rn(1.0f, x);
+}
+#else
+SVO_HD float rcp_rn(float x) { return div_rn(1.0f, x); }
+#endif
+
 // sin of a float through double precision, rounded once to float (the shading pass's liquid wobble,
 // low_res.frag:226): Cody-Waite reduction by pi/2 (k * PIO2_HI is exact for |k| < 2^20), Taylor
 // polynomials of sin / cos on [-pi/4, pi/4] (truncation < 3e-14), the quadrant's sign and function.
@@ -107,7 +123,7 @@ SVO_HD void cross3(const float a[3], const float b[3], float o[3]) {
 // glm::normalize: v * (1 / sqrt((x*x + y*y) + z*z))
 SVO_HD void normalize3(const float v[3], float o[3]) {
     float d = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2];
-    float r = div_rn(1.0f, sqrt_rn(d));
+    float r = rcp_rn(sqrt_rn(d));
     o[0] = v[0] * r;
     o[1] = v[1] * r;
     o[2] = v[2] * r;
@@ -165,7 +181,7 @@ struct Dda1 {
 SVO_HD Dda1 dda_axis(float o, float d) {
     Dda1 r;
     r.step = d < 0.0f ? -1 : 1;
-    double delta = (double)div_rn(1.0f, d);
+    double delta = (double)rcp_rn(d);
     r.adelta = delta >= 0.0 ? delta : -delta;
     r.cell = (int32_t)__builtin_truncf(o);
     double exact = (double)o;
