@@ -253,6 +253,9 @@ typedef struct {
    that are not linear then step voxel by voxel) */
 #define SVO_CAST_SEGMENTS 4096
 #define SVO_CAST_LINEAR_ONLY 8192
+/* svo_cast_desc.flags (results identical): frames whose rays all step with the same signs run an
+   instance with those signs compiled in; this bit keeps the per-wave sign flags instead */
+#define SVO_CAST_NO_OCTANT 16384
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

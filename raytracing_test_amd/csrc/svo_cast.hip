@@ -622,7 +622,12 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // ESCAPE (shading rays whose end position is not output): a ray moving up above the highest stored
 // voxel row `top` (wrapped) whose budget cannot carry it past the extent in y leaves the loop as a
 // miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off).
-template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, class Mem>
+// DIRS (1..8): every ray of the launch steps with the signs dirs_sign(DIRS, k) (frame_dirs proves it
+// on the host): the steps are compile-time constants and the sign branches of the crossings and brick
+// walks fold away; 0: per-wave sign flags (dir_flags)
+__host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
+
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1) {
@@ -654,7 +659,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     if (!SEG) fast = lin;
     const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
     uint32_t ud[3];
-    dir_flags(R.s, ud);
+    if (DIRS != 0) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            R.s[k] = dirs_sign(DIRS, k);  // (equal to dda_axis' step: frame_dirs)
+            ud[k] = dirs_sign(DIRS, k) > 0 ? 1u : 2u;
+        }
+    } else {
+        dir_flags(R.s, ud);
+    }
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
@@ -1004,7 +1017,7 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem
 }
 
 // WIDE: 64-bit node addresses (trees above kNarrowNodes nodes, or SVO_CAST_WIDE_ADDR)
-template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG>
+template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
@@ -1129,7 +1142,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS, false, false, SEG>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS, false, false, SEG, DIRS>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
@@ -1268,9 +1281,28 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
 // buffer offset reaches (or on request)
 bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap > kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
 
-// seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always)
+// seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always);
+// dirs: frame_dirs (the plain primary instance of narrow trees has one per sign octant)
+template <bool AO, bool SEG>
+void launch_dirs(int dirs, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
+    switch (dirs) {
+        case 1: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 1>), grid, block, 0, st, P); return;
+        case 2: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 2>), grid, block, 0, st, P); return;
+        case 3: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 3>), grid, block, 0, st, P); return;
+        case 4: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 4>), grid, block, 0, st, P); return;
+        case 5: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 5>), grid, block, 0, st, P); return;
+        case 6: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 6>), grid, block, 0, st, P); return;
+        case 7: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 7>), grid, block, 0, st, P); return;
+        default: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 8>), grid, block, 0, st, P); return;
+    }
+}
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
-void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
+void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, const CastParams& P, int dirs = 0) {
+    if (!STATS && !STAMPS && !SHADE && !wide && dirs) {  // (narrow trees: up to 2^28 nodes)
+        if (seg) launch_dirs<AO, true>(dirs, grid, block, st, P);
+        else launch_dirs<AO, false>(dirs, grid, block, st, P);
+        return;
+    }
     if (SHADE || seg) {
         if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, 0, st, P);
         else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false, true>), grid, block, 0, st, P);
@@ -1278,6 +1310,33 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
         if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, true, false>), grid, block, 0, st, P);
         else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, false, false>), grid, block, 0, st, P);
     }
+}
+
+// The launch's step-sign octant (1..8, dirs_sign) when every frame ray has the same step signs, else 0.
+// A pixel's direction before normalisation (raygen_pixel) is an affine function of the pixel, so its
+// extremes are at the frame's corners; a corner value beyond 1e-4 of the terms' magnitudes keeps
+// every pixel's rounded value (errors of a few ulps of those terms) on the same side of zero, and
+// normalisation keeps the sign.  Explicit rays: 0.
+static int frame_dirs(const CastParams& P) {
+    if (P.mode != MODE_FRAME || (P.flags & SVO_CAST_NO_OCTANT)) return 0;
+    int code = 1;
+    for (int a = 0; a < 3; a++) {
+        int pos = 0, neg = 0;
+        for (int c = 0; c < 4; c++) {
+            const int32_t px = (c & 1) ? P.width - 1 : 0, py = (c & 2) ? P.height - 1 : 0;
+            const float fx = ((float)px + 0.5f) * P.rg.rw, fy = ((float)py + 0.5f) * P.rg.rh;
+            const float sl = -(P.rg.ppx * (fx - 0.5f)), su = -fy + 0.5f;
+            const float lt = P.rg.l[a] * sl, ut = (P.rg.u[a] * su) * P.rg.ppy;
+            const float v = (P.rg.c[a] + lt) + ut;
+            const float mag = fabsf(P.rg.c[a]) + fabsf(P.rg.l[a]) * fabsf(P.rg.ppx) + fabsf(P.rg.u[a] * P.rg.ppy);
+            if (v > 1e-4f * mag) pos++;
+            else if (v < -1e-4f * mag) neg++;
+        }
+        if (pos == 4) continue;
+        if (neg == 4) code += 1 << a;
+        else return 0;
+    }
+    return code;
 }
 
 // Can the launch hold rays that are not linear (svo_cast.hip, "Exact closed-form skipping")?  From an
@@ -1579,13 +1638,13 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     const bool wide = wide_nodes(t, d->flags), seg = need_seg(P);
     if (P.ao_n > 0) {
         if (P.flags & SVO_CAST_STATS) launch_cast<true, true, true, false>(wide, seg, grid, block, st, P);
-        else launch_cast<false, false, true, false>(wide, seg, grid, block, st, P);
+        else launch_cast<false, false, true, false>(wide, seg, grid, block, st, P, frame_dirs(P));
     } else if (P.flags & SVO_CAST_STATS) {
         launch_cast<true, true, false, false>(wide, seg, grid, block, st, P);
     } else if (P.flags & SVO_CAST_TIMELINE) {
         launch_cast<false, true, false, false>(wide, seg, grid, block, st, P);
     } else {
-        launch_cast<false, false, false, false>(wide, seg, grid, block, st, P);
+        launch_cast<false, false, false, false>(wide, seg, grid, block, st, P, frame_dirs(P));
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;

@@ -66,7 +66,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
     for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST,
-                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_LINEAR_ONLY):
+                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_LINEAR_ONLY, rt.CAST_NO_OCTANT):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -375,7 +375,7 @@ def test_depth12_fractional_camera(rt, oracle_mod, depth12, org):
     assert np.array_equal(sub["pos"], ref["pos"]) and np.array_equal(sub["steps"], ref["steps"])
     assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
     assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
-    for flags in (rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY):
+    for flags in (rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY, rt.CAST_NO_OCTANT):
         o2 = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384, flags=flags))
         for k in out:
             assert np.array_equal(out[k], o2[k]), (k, flags)
@@ -391,10 +391,12 @@ def test_depth12_full_frame_properties(rt, depth12):
     b = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384))
     c = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_ITERATIVE))
     e = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_WIDE_ADDR))
+    f = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_NO_OCTANT))
     for k in a:
         assert np.array_equal(a[k], b[k]), k
         assert np.array_equal(a[k], c[k]), k
         assert np.array_equal(a[k], e[k]), k
+        assert np.array_equal(a[k], f[k]), k
     rng = np.random.default_rng(9)
     idx = rng.integers(0, len(a["hit"]), 20000)
     ids = depth12.get_blocks(a["pos"][idx])
