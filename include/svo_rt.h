@@ -248,11 +248,9 @@ typedef struct {
    small enough for 32-bit buffer offsets (trees of more than 2^28 nodes always use them) */
 #define SVO_CAST_WIDE_ADDR 2048
 /* svo_cast_desc.flags (results identical): the kernel instance picks itself by the origins — from
-   integral origins every ray's crossings are exact linear sums; other rays cross empty regions in
-   exact segments.  SEGMENTS forces the segment-capable instance, LINEAR_ONLY the other (where rays
-   that are not linear then step voxel by voxel) */
+   integral or half-integral origins every ray's crossings are exact linear sums; other rays cross
+   empty regions in exact segments.  SEGMENTS forces the segment-capable instance for any origin */
 #define SVO_CAST_SEGMENTS 4096
-#define SVO_CAST_LINEAR_ONLY 8192
 /* svo_cast_desc.flags (results identical): frames whose rays all step with the same signs run an
    instance with those signs compiled in; this bit keeps the per-wave sign flags instead */
 #define SVO_CAST_NO_OCTANT 16384

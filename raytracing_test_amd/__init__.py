@@ -42,7 +42,6 @@ CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel
 CAST_HORIZON_FIRST = 1024  # scheduling: tile rows with the shallowest centre ray first
 CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (results identical)
 CAST_SEGMENTS = 4096  # force the kernel instance with segment-exact crossings (results identical)
-CAST_LINEAR_ONLY = 8192  # force the instance without them: non-linear rays step voxel by voxel (results identical)
 CAST_NO_OCTANT = 16384  # per-wave step-sign flags instead of the launch's compiled-in sign octant (results identical)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",

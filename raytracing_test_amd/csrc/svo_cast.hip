@@ -553,7 +553,10 @@ __device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) 
 // `left` = per-axis steps left in the brick (bytes 0-2, a zero byte = left the brick), `solid` =
 // stopped on a solid voxel.  The crossing value of every step is kept (recovering it after the
 // walk as T - a, exact for fast rays, measured no faster).
-template <bool STATS>
+// TRACK: keep the crossing value of every step (R.tlast); without it trace recovers the last one
+// once, at the end of the ray (exact sums: T - a).  (A wave-uniform runtime flag in this loop
+// measured 1.6 % slower than tracking always.)
+template <bool STATS, bool TRACK>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
     // 127 - voxel index (byte 0: the 64-bit shift reads its low 6 bits, 63 - v, which moves the
@@ -571,7 +574,7 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
             // one DDA step (ray_caster.cpp:70-80) without position updates
             const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
             const bool cy = !cx && (R.T[1] < R.T[2]);
-            R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            if (TRACK) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
             R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
             R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
             R.T[2] = (cx || cy) ? R.T[2] : R.T[2] + R.a(2);  // (a mask or, not a fourth f64 compare)
@@ -651,13 +654,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     bool fast = ((unsigned)!(P.flags & SVO_CAST_ITERATIVE) & (unsigned)(budget < (1 << 20)) & (unsigned)axis_ok(R.T[0], R.a(0)) &
                  (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2))) != 0u;
     // SEG: the instance carries segment-bounded crossings (the host picks it when rays can be
-    // non-linear: need_seg).  The other one takes closed-form crossings only for rays that are
-    // linear by a cheap sufficient test (lin_origin) and steps any other ray voxel by voxel: the same
-    // results either way, and the linear waves keep the shorter code.
+    // non-linear: need_seg).  The other one runs exact-origin rays only; it re-tests them cheaply
+    // (lin_origin) and steps any other ray voxel by voxel.
     bool lin = SEG ? fast && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) && exact_axis(R.T[2], R.a(2), budget)
                    : ((unsigned)fast & (unsigned)lin_origin(o[0]) & (unsigned)lin_origin(o[1]) & (unsigned)lin_origin(o[2])) != 0u;
     if (!SEG) fast = lin;
     const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
+    // Instances without segments run rays from integral / half-integral origins only (need_seg):
+    // every sum they take is exact, so they recover the output crossing value once at the end
+    // (T - a on the last step's axis) instead of keeping it on every brick step
+    constexpr bool TRACK = REFLECT || SEG;
     uint32_t ud[3];
     if (DIRS != 0) {
 #pragma unroll
@@ -751,7 +757,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             const uint32_t left0 = (((w[0] & 3u) | ((w[1] & 3u) << 8) | ((w[2] & 3u) << 16)) ^ up3) + 0x010101u;
             uint32_t left, v;
             bool solid;
-            v = brick_walk<STATS>(R, bmask, w, left0, left, solid, st);
+            v = brick_walk<STATS, TRACK>(R, bmask, w, left0, left, solid, st);
             if (solid) {
                 mat = brick_material(mats, bmask, bref, binfo, v);
                 done = true;
@@ -894,6 +900,13 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
         if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
+    }
+    if (!TRACK && R.axis < 3u) {
+        // the last step's crossing: T - a exactly (exact sums); an infinite absDelta only comes
+        // with an infinite crossing (deltaPos = inf - frac * inf), which stays inf
+        const double Ta = R.axis == 0u ? R.T[0] : (R.axis == 1u ? R.T[1] : R.T[2]);
+        const float aa = R.axis == 0u ? R.af[0] : (R.axis == 1u ? R.af[1] : R.af[2]);
+        R.tlast = (float)(__builtin_isinf(aa) ? Ta : Ta - (double)aa);
     }
     Hit h;
     h.x = R.r[0];
@@ -1340,12 +1353,12 @@ static int frame_dirs(const CastParams& P) {
 }
 
 // Can the launch hold rays that are not linear (svo_cast.hip, "Exact closed-form skipping")?  From an
-// integral or half-integral origin every ray is (lin_origin); explicit rays are not inspected.
-// Either instance gives the same results: this only picks the faster one.
+// integral or half-integral origin every ray is (lin_origin, with budgets below 2^28 every sum it
+// takes is exact); explicit rays are not inspected.  The instance without segments relies on it
+// (trace: TRACK); SVO_CAST_SEGMENTS forces the other one (the same results).
 static bool need_seg(const CastParams& P) {
-    if (P.flags & (SVO_CAST_ITERATIVE | SVO_CAST_LINEAR_ONLY)) return false;
     if (P.flags & SVO_CAST_SEGMENTS) return true;
-    if (P.mode == MODE_EXPLICIT) return true;
+    if (P.mode == MODE_EXPLICIT || P.steps >= (1 << 28)) return true;
     const int32_t nf = P.mode == MODE_FRAME ? P.n_frames : 1;
     const float* org = P.mode == MODE_FRAME ? P.frame_org : P.org;
     for (int32_t i = 0; i < 3 * nf; i++)

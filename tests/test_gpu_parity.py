@@ -66,7 +66,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
     for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_HORIZON_FIRST,
-                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_LINEAR_ONLY, rt.CAST_NO_OCTANT):
+                  rt.CAST_XCD_SWIZZLE, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_NO_OCTANT, rt.CAST_SEGMENTS | rt.CAST_ITERATIVE):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -132,7 +132,7 @@ def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
     dirs = np.array([c[1] for c in cases], np.float32)
     for steps in sorted(set(c[2] for c in cases)):
         sel = [i for i, c in enumerate(cases) if c[2] == steps]
-        for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR, rt.CAST_LINEAR_ONLY):
+        for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR):
             out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps, flags)
             compare(rt, gtree, out, ref, "edge S=%d flags=%d" % (steps, flags))
 
@@ -166,7 +166,7 @@ def test_random_rays(rt, torch_cuda, gtree, ref_world_oracle):
     # octant box [-256, 0)^3 for these origins
     keep = ~_segment_hits_box(org, d, 301.0, np.full(3, -256.0), np.zeros(3))
     org, d = org[keep], d[keep]
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY):
+    for flags in (0, rt.CAST_ITERATIVE):
         out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, org, d, 300, flags)
         compare(rt, gtree, out, ref, "random flags=%d" % flags)
 
@@ -375,7 +375,7 @@ def test_depth12_fractional_camera(rt, oracle_mod, depth12, org):
     assert np.array_equal(sub["pos"], ref["pos"]) and np.array_equal(sub["steps"], ref["steps"])
     assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
     assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
-    for flags in (rt.CAST_ITERATIVE, rt.CAST_LINEAR_ONLY, rt.CAST_NO_OCTANT):
+    for flags in (rt.CAST_ITERATIVE, rt.CAST_NO_OCTANT):
         o2 = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384, flags=flags))
         for k in out:
             assert np.array_equal(out[k], o2[k]), (k, flags)
