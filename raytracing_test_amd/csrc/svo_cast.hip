@@ -356,7 +356,8 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
     for (int k = 0; k < 3; k++) E[k] = on_grid(R.T[k], e[k], R.a(k));
     // lexicographic minimum of (E, rank) with rank z < y < x (the DDA rule applied to exits)
     // exit flags as lane masks (SGPRs): selects and tie terms read them directly
-    const uint64_t mx = __ballot((E[0] < E[1]) && (E[0] < E[2]));
+    // (ballots of single compares are the compare masks themselves)
+    const uint64_t mx = __ballot(E[0] < E[1]) & __ballot(E[0] < E[2]);
     const uint64_t my = __ballot(E[1] < E[2]) & ~mx;
     const double V = sel64(mx, E[0], sel64(my, E[1], E[2]));
     // Events of another axis k that precede the exit event: T + j*a < V when k loses ties
@@ -378,7 +379,9 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
-        R.r[k] += __mul24(R.s[k], n[k]);  // 24-bit multiply-add: full rate (s = +-1, |n| < 2^21)
+        // a compile-time step (sign octant instances) adds or subtracts; else a 24-bit multiply-add
+        // (full rate; s = +-1, |n| < 2^21)
+        R.r[k] += __builtin_constant_p(R.s[k]) ? (R.s[k] > 0 ? n[k] : -n[k]) : __mul24(R.s[k], n[k]);
     }
     R.tlast = (float)V;
     R.axis = sel32(mx, 0u, sel32(my, 1u, 2u));
@@ -556,6 +559,8 @@ __device__ __forceinline__ void wrap3(const Ray& R, uint32_t wm, uint32_t w[3]) 
 // TRACK: keep the crossing value of every step (R.tlast); without it trace recovers the last one
 // once, at the end of the ray (exact sums: T - a).  (A wave-uniform runtime flag in this loop
 // measured 1.6 % slower than tracking always.)
+// (Skipping the per-step budget test for waves with budget for a whole walk, at most 10 steps,
+// measured equal.)
 template <bool STATS, bool TRACK>
 __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uint32_t w[3], uint32_t left0, uint32_t& left, bool& solid,
                                                Stats& st) {
