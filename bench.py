@@ -63,6 +63,9 @@ CONFIGS = {
     "c3": dict(levels=6, cols=4096, W=1920, H=1080, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
                label="C3: depth-12 SVO (4096^2 terrain columns, 6 levels, 4096^3), 1920x1080", bray="C3",
                metric="primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
+    "c3f": dict(levels=6, cols=4096, W=1920, H=1080, origin=(4.37, 90.61, 4.23), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
+                label="C3 from a non-integral camera position (segment-exact crossings): depth-12 SVO, 1920x1080", bray="C3f",
+                metric="primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
     "c5": dict(levels=7, cols=16384, W=3840, H=2160, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
                label="C5: depth-14 SVO (16384^2 terrain columns, 7 levels, 16384^3), 3840x2160", bray="C5",
                metric="primary rays/sec at 4K, depth-14 SVO; achieved HBM GB/s vs roofline"),

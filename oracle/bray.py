@@ -2,7 +2,8 @@
 B_ray = 16*E_node + 4*E_child + B_out with E_node = E_child + 1, where E_child counts node entries
 along the reference DDA path under the shader's common-ancestor restart (low_res.frag:493-531) on
 the reference-format tree.  Writes profiles/bray.json, which bench.py reads (it never imports the
-oracle for this).  Usage: python oracle/bray.py
+oracle for this).  Usage: python oracle/bray.py [C3f]  (C3f: only the non-integral-camera C3 entry,
+merged into the existing file)
 """
 import json
 import os
@@ -17,7 +18,24 @@ from oracle import oracle as O  # noqa: E402
 B_OUT = 24
 
 
+C3F_ORIGIN = (4.37, 90.61, 4.23)  # bench.py CONFIGS["c3f"]
+
+
+def c3f_entry():
+    t = O.Tree.terrain(6, 4096, 4096)
+    e = t.frame_entries(C3F_ORIGIN, O.normalize((1, -0.45, 1)), 1920, 1080, 16384, nthreads=8) / (1920 * 1080)
+    return {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
+            "tree": "as C3, camera at %s (non-integral: segment-exact crossings)" % (C3F_ORIGIN,)}
+
+
 def main():
+    if sys.argv[1:] == ["C3f"]:
+        path = os.path.join(ROOT, "profiles", "bray.json")
+        res = json.load(open(path))
+        res["C3f"] = c3f_entry()
+        json.dump(res, open(path, "w"), indent=1)
+        print(json.dumps(res["C3f"], indent=1))
+        return
     res = {"formula": "B_ray = 16*(E_child+1) + 4*E_child + B_out, B_out = %d (this build's hit record)" % B_OUT,
            "source": "oracle/bray.py (orc_frame_entries, oracle/oracle.c)"}
     ref = O.Tree.reference_world()
@@ -29,6 +47,7 @@ def main():
     e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, nthreads=8) / (1920 * 1080)
     res["C3"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
                  "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
+    res["C3f"] = c3f_entry()
     # C4: §8(d) "for AO: add <= 5 steps x E per sample" -- the AO rays' node entries (each continues the
     # restart model from the primary's final lookup), 16 + 4 B per entry, per primary ray of the frame;
     # B_OUT grows by the 1-B AO count

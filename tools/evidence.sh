@@ -10,6 +10,7 @@ step() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; "$@"; local 
 b() { local name=$1; shift; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python bench.py "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_$name.err; exit $rc; }; cut -c1-300 $OUT/bench_$name.json; }
 d() { local name=$1 n=$2 port=$3; shift 3; echo "[evidence] $(date +%T) $name"; timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $port bench.py --gpus $n --dist-backend gloo "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$name.err; exit $rc; }; grep '^{' $OUT/bench_$name.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['n_gpus'], d['scaling'], round(d['value']/1e6,1), 'M rays/s', 'verified', d.get('gather_verified'))"; }
 b c3
+b c3f --config c3f
 b c1 --config c1
 b c4_ao16 --ao 16
 b c4_ao20 --ao 20 --no-cpu-baseline
@@ -25,7 +26,8 @@ d g2_strong 2 29542 --steps 4 --warmup 1 --frames 1 --verify
 d g3_f2 3 29543 --steps 4 --warmup 1 --frames 2 --verify
 d g2_ao 2 29544 --steps 4 --warmup 1 --ao 16 --verify
 d g2_shade 2 29545 --steps 4 --warmup 1 --shade
-step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/prof.err
-step rocprof_c5 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c5.json 2> $OUT/prof_c5.err
-step rocprof_c4 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- python3 bench.py --ao 16 --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_c4.json 2> $OUT/prof_c4.err
-step rocprof_shade timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_shade -o run -- python3 bench.py --shade --steps 10 --warmup 2 --no-cpu-baseline > $OUT/bench_prof_shade.json 2> $OUT/prof_shade.err
+step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof.json 2> $OUT/prof.err
+step rocprof_c5 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_c5.json 2> $OUT/prof_c5.err
+step rocprof_c4 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- python3 bench.py --ao 16 --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_c4.json 2> $OUT/prof_c4.err
+step rocprof_c3f timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c3f -o run -- python3 bench.py --config c3f --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_c3f.json 2> $OUT/prof_c3f.err
+step rocprof_shade timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_shade -o run -- python3 bench.py --shade --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_shade.json 2> $OUT/prof_shade.err

@@ -15,7 +15,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
   i=$((i+1))
   echo "[pmc] pass $i: $grp"
   timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d "$OUT/pmc_$i" -o run -- \
-      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pmc_$i.log" 2>&1
+      python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --pipelined-steps 0 "$@" > "$OUT/pmc_$i.log" 2>&1
   rc=$?
   echo "rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/pmc_$i.log"; exit $rc; fi

@@ -7,6 +7,7 @@ TAG=${1:-pmcall}
 run() { local key=$1; shift; echo "[pmc_all] $(date +%T) $key"; timeout -k 10 900 bash tools/pmc.sh ${TAG}_$key "$@" > gpurun_out/${TAG}_$key.log 2>&1; local rc=$?; echo "$key rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_$key.log; exit $rc; }; }
 mkdir -p gpurun_out
 run c3
+run c3f --config c3f
 run c3_ao16 --ao 16
 run c5 --config c5
 run c3_shade --shade
