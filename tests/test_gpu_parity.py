@@ -409,6 +409,32 @@ def test_depth12_full_frame_properties(rt, depth12):
     assert np.array_equal(l1[a["hit"]], used[a["hit"]])
 
 
+@pytest.mark.parametrize("octant", range(8))
+def test_octant_frames(rt, gtree, ref_world_oracle, octant):
+    """Frames whose rays all step with one sign octant run an instance with the signs compiled in
+    (svo_cast.hip: frame_dirs); every octant, integral and fractional origins, against the oracle and
+    against the per-wave sign flags (SVO_CAST_NO_OCTANT)."""
+    sx, sy, sz = [(-1.0 if (octant >> k) & 1 else 1.0) for k in range(3)]
+    dn = rt.normalize([sx * 1.0, sy * 0.45, sz * 0.8])
+    W, H = 96, 64
+    for org in ((128.0, 60.0, 128.0), (131.3, 58.7, 125.45)):
+        ref = ref_world_oracle.cast_frame(org, dn, W, H, 300, ppx=0.6, ppy=0.4)
+        for flags in (0, rt.CAST_NO_OCTANT):
+            out = gtree.cast_frame(org, dn, W, H, 300, ppx=0.6, ppy=0.4, flags=flags)
+            compare(rt, gtree, out, ref, "octant %d org %s flags %d" % (octant, org, flags))
+
+
+def test_ao_fractional_origin(rt, gtree, ref_world_oracle):
+    """AO (C4) from a non-integral camera: the AO instance with segment-exact primaries (and its
+    sign-octant form) against the oracle's AO counts."""
+    org, dn = (40.25, 70.5, 33.75), rt.normalize([1.0, -0.5, 0.7])
+    ao, hit = ref_world_oracle.cast_frame_ao(org, dn, 128, 96, 300, 16, 5)
+    for flags in (0, rt.CAST_NO_OCTANT):
+        out = rt.decode_hits(gtree.cast_frame(org, dn, 128, 96, 300, ao_samples=16, ao_steps=5, flags=flags))
+        assert np.array_equal(out["hit"], hit != 0)
+        assert np.array_equal(out["ao"], ao), flags
+
+
 @pytest.mark.parametrize("n_ao", [16, 20])
 def test_ao_reference_world(rt, gtree, ref_world_oracle, n_ao):
     """A8 / C4: hemisphere AO counts (per pixel, rays that hit within 5 steps) against the oracle,
