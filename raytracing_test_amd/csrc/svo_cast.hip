@@ -442,13 +442,16 @@ struct Parent {
 // trees — the builders accept up to 2^32 nodes, 64 GiB — through 64-bit global addresses.  The host
 // picks the instance per tree (svo_cast.hip: node_addressing), so no index can wrap or fall outside
 // the resource and read zeros (an empty node) silently.
-constexpr uint64_t kNarrowNodes = 1ull << 28;  // ni << 4 stays below 2^32
+// Loads take "one past" indices: ni1 = node index + 1 = first child + rank + 1, which is the popcount
+// of the child mask shifted so the child's own bit stays in (slot_top: no further shift), and the
+// bases sit one node before the array.
+constexpr uint64_t kNarrowNodes = 1ull << 28;  // below it, ni1 << 4 stays below 2^32
 
 struct BufNodes {
     __amdgpu_buffer_rsrc_t rsrc;
     __device__ __forceinline__ explicit BufNodes(const Node* p)
-        : rsrc(__builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(p), (short)0, (int)0xFFFFFFFFu, (int)0x00020000)) {}
-    __device__ __forceinline__ Node load(uint32_t ni) const {
+        : rsrc(__builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(p - 1), (short)0, (int)0xFFFFFFFFu, (int)0x00020000)) {}
+    __device__ __forceinline__ Node load(uint32_t ni) const {  // node ni - 1
         const uint32_t off = ni << 4;
         Node n;
         n.mask = ((uint64_t)(uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0)) |
@@ -462,8 +465,8 @@ struct BufNodes {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct WideNodes {
     const __attribute__((address_space(1))) u32x4* p;
-    __device__ __forceinline__ explicit WideNodes(const Node* q) : p((const __attribute__((address_space(1))) u32x4*)q) {}
-    __device__ __forceinline__ Node load(uint32_t ni) const {
+    __device__ __forceinline__ explicit WideNodes(const Node* q) : p((const __attribute__((address_space(1))) u32x4*)(q - 1)) {}
+    __device__ __forceinline__ Node load(uint32_t ni) const {  // node ni - 1
         const u32x4 v = p[ni];  // 64-bit address: base + (u64)ni * 16
         Node n;
         n.mask = (uint64_t)v.x | ((uint64_t)v.y << 32);
@@ -500,7 +503,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
             if (STATS) st.cache_empty++;
             return R_EMPTY;
         }
-        ni = popc_add(t << 1, par.ref);
+        ni = popc_add(t, par.ref);  // (one past: BufNodes)
         dd = P.levels - (int32_t)(par.sh >> 1);  // depth of that child
         if (STATS && dd == 0) st.root_starts++;
     }
@@ -528,7 +531,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
             par.sh = sh;
             const uint64_t t = slot_top(n.mask, child_slot(w[0], w[1], w[2], sh));
             const bool occ = (int64_t)t < 0;
-            ni = popc_add(t << 1, n.ref);
+            ni = popc_add(t, n.ref);
             dd++;
             more = occ && dd < P.levels;
             sh_out = occ ? 0u : sh;  // (occupied at the last level only in a malformed tree: one voxel)
@@ -986,7 +989,7 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& m
         more = false;
         const uint64_t t = slot_top(mask, child_slot(w[0], w[1], w[2], sh));
         if ((int64_t)t < 0) {
-            const Node n = mem.load(popc_add(t << 1, ref));
+            const Node n = mem.load(popc_add(t, ref));
             const uint32_t kind = n.info & K_KIND_MASK;
             if (kind == K_INTERIOR) {
                 mask = n.mask;
@@ -1297,7 +1300,7 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
 
 // node addressing of a cast over t: 64-bit when its device allocation holds more nodes than a 32-bit
 // buffer offset reaches (or on request)
-bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap > kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
+bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap >= kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
 
 // seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always);
 // dirs: frame_dirs (the plain primary instance of narrow trees has one per sign octant)
