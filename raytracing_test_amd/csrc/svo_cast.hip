@@ -476,7 +476,11 @@ struct WideNodes {
     }
 };
 
-template <bool STATS, class Mem>
+// SPLIT: the levels above the bricks hold interior nodes or SOLID regions only; a SOLID region ends
+// the ray, so the parent may be overwritten by it, and those levels need no leaf branch and no
+// copies of the loaded node (instances whose callers read the final parent — AO's brick_near, the
+// shading pass's uniform regions — keep the general loop)
+template <bool STATS, bool SPLIT, class Mem>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, const Path& path,
                                            const uint32_t w[3], uint32_t moved, Parent& par, uint32_t& sh_out, uint64_t& bmask,
                                            uint32_t& bref, uint32_t& binfo, Stats& st) {
@@ -509,6 +513,46 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
     }
     // descend (one exit: no per-exit register copies)
     uint32_t res = R_EMPTY;
+    if (SPLIT) {
+        bool pend = true;  // node ni - 1 occupies the cell and is not loaded yet
+        bool more = dd < P.levels - 1;
+        while (more) {
+            if (STATS) {
+                st.wv_descents += wave_lead();
+                st.loads++;
+            }
+            const Node n = mem.load(ni);
+            const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
+            path.mask[dd * kBlock] = n.mask;
+            path.ref[dd * kBlock] = n.ref;
+            par.mask = n.mask;
+            par.ref = n.ref;
+            par.sh = sh;
+            binfo = n.info;
+            const uint64_t t = slot_top(n.mask, child_slot(w[0], w[1], w[2], sh));
+            const bool occ = (int64_t)t < 0;
+            const bool solid = (n.info & K_KIND_MASK) == K_SOLID;
+            ni = popc_add(t, n.ref);
+            dd++;
+            pend = occ && !solid;
+            more = pend && dd < P.levels - 1;
+            sh_out = occ ? 0u : sh;
+            res = solid ? R_SOLID : R_EMPTY;
+        }
+        if (pend) {  // the brick level: a BRICK or SOLID leaf
+            if (STATS) {
+                st.wv_descents += wave_lead();
+                st.loads++;
+            }
+            const Node n = mem.load(ni);
+            bmask = n.mask;
+            bref = n.ref;
+            binfo = n.info;
+            sh_out = 2u;
+            res = (n.info & K_KIND_MASK) == K_SOLID ? R_SOLID : R_BRICK;
+        }
+        return res;
+    }
     bool more = dd < P.levels;
     while (more) {
         if (STATS) {
@@ -638,7 +682,7 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // walks fold away; 0: per-wave sign flags (dir_flags)
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
-template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, class Mem>
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1) {
@@ -724,7 +768,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
-        const uint32_t kind = lookup<STATS>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
+        const uint32_t kind = lookup<STATS, !REFLECT && !KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
@@ -1163,7 +1207,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS, false, false, SEG, DIRS>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS, false, false, SEG, DIRS, AO>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
