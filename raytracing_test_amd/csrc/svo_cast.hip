@@ -425,10 +425,22 @@ enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
 // the descent at most one level down; leaving the parent's region restarts at the root, whose top
 // levels are staged in LDS.
-// per-lane path of the last descent in LDS (element [depth * kBlock])
+// per-lane path of the last descent in LDS
 struct Path {
-    uint64_t* __restrict__ mask;
-    uint32_t* __restrict__ ref;
+    // [depth][mask low, mask high, first child][lane] dwords: one address per depth (the three
+    // words at +0, +256, +512 bytes: ds_write2st64 / ds_read2st64 and one more)
+    uint32_t* __restrict__ w;
+    __device__ __forceinline__ void put(int32_t d, uint64_t mask, uint32_t ref) const {
+        uint32_t* e = w + d * (3 * kBlock);
+        e[0] = (uint32_t)mask;
+        e[kBlock] = (uint32_t)(mask >> 32);
+        e[2 * kBlock] = ref;
+    }
+    __device__ __forceinline__ uint64_t mask(int32_t d) const {
+        const uint32_t* e = w + d * (3 * kBlock);
+        return (uint64_t)e[0] | ((uint64_t)e[kBlock] << 32);
+    }
+    __device__ __forceinline__ uint32_t ref(int32_t d) const { return w[d * (3 * kBlock) + 2 * kBlock]; }
 };
 
 struct Parent {
@@ -496,8 +508,8 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
             // holds this cell (depth levels-1-floor(h/2), h = highest differing bit) becomes the
             // parent, read back from the per-lane path in LDS
             const int32_t da = P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1);  // (diff != 0)
-            par.mask = path.mask[da * kBlock];
-            par.ref = path.ref[da * kBlock];
+            par.mask = path.mask(da);
+            par.ref = path.ref(da);
             par.sh = (uint32_t)(2 * (P.levels - 1 - da));
             if (STATS) st.path_starts++;
         }
@@ -523,8 +535,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
             }
             const Node n = mem.load(ni);
             const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
-            path.mask[dd * kBlock] = n.mask;
-            path.ref[dd * kBlock] = n.ref;
+            path.put(dd, n.mask, n.ref);
             par.mask = n.mask;
             par.ref = n.ref;
             par.sh = sh;
@@ -568,8 +579,7 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
         binfo = n.info;
         if (kind == K_INTERIOR) {
             const uint32_t sh = (uint32_t)(2 * (P.levels - 1 - dd));
-            path.mask[dd * kBlock] = n.mask;
-            path.ref[dd * kBlock] = n.ref;
+            path.put(dd, n.mask, n.ref);
             par.mask = n.mask;
             par.ref = n.ref;
             par.sh = sh;
@@ -1024,8 +1034,8 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& m
                                                const uint32_t hw[3], int32_t dmax) {
     const uint32_t diff = ((w[0] ^ hw[0]) | (w[1] ^ hw[1]) | (w[2] ^ hw[2])) | 1u;
     const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1), dmax);  // (diff != 0)
-    uint64_t mask = path.mask[da * kBlock];
-    uint32_t ref = path.ref[da * kBlock];
+    uint64_t mask = path.mask(da);
+    uint32_t ref = path.ref(da);
     uint32_t sh = (uint32_t)(2 * (P.levels - 1 - da));
     uint64_t res = 0ull;
     bool more = true;
@@ -1095,9 +1105,8 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     if (STAMPS && threadIdx.x == 0) t_start = __builtin_amdgcn_s_memrealtime();
     // per-lane node path (mask and first-child index of the interior node at each depth of the
     // last descent), [depth][lane]
-    __shared__ uint64_t path_mask[(kMaxLevels - 1) * kBlock];
-    __shared__ uint32_t path_ref[(kMaxLevels - 1) * kBlock];
-    const Path path = {path_mask + threadIdx.x, path_ref + threadIdx.x};
+    __shared__ uint32_t path_words[(kMaxLevels - 1) * 3 * kBlock];
+    const Path path = {path_words + threadIdx.x};
     // hemisphere AO sample set, broadcast from LDS
     __shared__ float ao_tab[3 * 64];
     if (AO)
