@@ -618,8 +618,9 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
                                                Stats& st) {
     // 127 - voxel index (byte 0: the 64-bit shift reads its low 6 bits, 63 - v, which moves the
     // voxel's bit to bit 63 — one shift and a sign test; the +-1/4/16 moves of a walk stay within
-    // 48..143, so byte 0 never borrows) and steps left (bytes 1-3) in one register.  The step keeps
-    // its delta instead of the axis: the axis follows from the last delta after the walk.
+    // 48..143, so byte 0 never borrows) and steps left (bytes 1-3, biased: 0x80 + left - 1, so a
+    // byte leaves the brick by clearing its top bit, without a borrow) in one register.  The step
+    // keeps its delta instead of the axis: the axis follows from the last delta after the walk.
     uint32_t pk = (left0 << 8) | (127u - child_slot(w[0], w[1], w[2], 0u));
     const uint32_t d0 = (uint32_t)(-R.s[0]) - 0x100u, d1 = (uint32_t)(-R.s[1] * 4) - 0x10000u, d2 = (uint32_t)(-R.s[2] * 16) - 0x1000000u;
     uint32_t dl = 0u;
@@ -642,7 +643,7 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
                 st.brick_steps++;
                 st.wv_brick += wave_lead();
             }
-            go = ((pk - 0x01010100u) & ~pk & 0x80808000u) == 0u;  // no steps-left byte at 0: inside
+            go = (pk & 0x80808000u) == 0x80808000u;  // every steps-left byte above its bias: inside
         }
     } while (go);
     if (dl != 0u) R.axis = dl == d0 ? 0u : (dl == d1 ? 1u : 2u);
@@ -809,16 +810,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // Voxel index v and per-axis steps left in the brick (one byte each) are stepped
             // instead of positions; positions follow from the step counts when the brick ends.
             // Steps left: 4 - c stepping up, c + 1 stepping down (c = the cell in the brick), i.e.
-            // (c ^ 3) + 1 or c + 1 — all three bytes at once.
+            // (c ^ 3) + 1 or c + 1 — all three bytes at once, biased by 0x7F (brick_walk).
             const uint32_t up3 = (R.s[0] > 0 ? 3u : 0u) | (R.s[1] > 0 ? 0x300u : 0u) | (R.s[2] > 0 ? 0x30000u : 0u);
-            const uint32_t left0 = (((w[0] & 3u) | ((w[1] & 3u) << 8) | ((w[2] & 3u) << 16)) ^ up3) + 0x010101u;
+            const uint32_t left0 = (((w[0] & 3u) | ((w[1] & 3u) << 8) | ((w[2] & 3u) << 16)) ^ up3) + 0x808080u;
             uint32_t left, v;
             bool solid;
             v = brick_walk<STATS, TRACK>(R, bmask, w, left0, left, solid, st);
             if (solid) {
                 mat = brick_material(mats, bmask, bref, binfo, v);
                 done = true;
-            } else if (R.steps <= 0 && (((left - 0x010101u) & ~left & 0x808080u) == 0u)) {
+            } else if (R.steps <= 0 && (left & 0x808080u) == 0x808080u) {
                 done = true;  // budget ended inside the brick
             }
             const uint32_t dn = left0 - left;  // steps taken per axis, one byte each (no borrows)
