@@ -337,6 +337,7 @@ __device__ __forceinline__ int32_t seg_cap(double T, float af, float inva) {
 // the wave holds rays that are not linear): each axis' exit event is also held to its exact segment (seg_cap); an exit on such a
 // bound is a virtual one inside the box (the next lookup finds the same empty cell in the parent's
 // mask, without a load, and the crossing continues).
+template <bool TRACK = true>
 __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) {
     // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
@@ -378,7 +379,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
         // (full rate; s = +-1, |n| < 2^21)
         R.r[k] += __builtin_constant_p(R.s[k]) ? (R.s[k] > 0 ? n[k] : -n[k]) : __mul24(R.s[k], n[k]);
     }
-    R.tlast = (float)V;
+    if (TRACK) R.tlast = (float)V;  // (else recovered at the end of the ray: trace)
     R.axis = sel32(mx, 0u, sel32(my, 1u, 2u));
     R.steps -= total;
     return true;
@@ -752,7 +753,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         wrap3(R, wm, w);
         if ((int32_t)w[1] > pre_top) {
             const int32_t ex[3] = {R.steps, R.s[1] < 0 ? (int32_t)w[1] - pre_top - 1 : (int32_t)(wm - w[1]), R.steps};
-            skip_box(R, ex, wseg);
+            skip_box<TRACK>(R, ex, wseg);
         }
     }
     // one back-edge: every path through the body ends at the loop latch
@@ -787,7 +788,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
                        box_exits(w, R.s, sh, par.mask, ud, ex);
-                       return skip_box(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
+                       return skip_box<TRACK>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                    }())) {
             if (STATS && fast) st.skip_out++;
             if (fast) {
