@@ -261,6 +261,9 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
         })
     elif model:
         roof["bound"] = "hbm"  # the §8(d) model's bound; no counters committed for this config
+    if roof["frac"] is not None and roof["frac"] > 1.0:
+        roof["note"] = ("the §8(d) algorithmic bytes exceed the HBM peak: the nodes they count are served from L2 / MALL "
+                        "(the measured HBM traffic is hbm_gbs_measured)")
     return roof
 
 
