@@ -1204,7 +1204,8 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                     // shadow ray towards the sun from the centre of lastPos, through empty and liquid
                     const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                          (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                    dark = (trace<false, false, true>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
+                    // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
+                    dark = (trace<false, false, true, false, DIRS>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                                 .info & HIT_BIT) != 0u;
                 }
             }
@@ -1369,10 +1370,22 @@ void launch_dirs(int dirs, dim3 grid, dim3 block, hipStream_t st, const CastPara
 }
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
 void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, const CastParams& P, int dirs = 0) {
-    if (!STATS && !STAMPS && !SHADE && !wide && dirs) {  // (narrow trees: up to 2^28 nodes)
+    if (!STATS && !STAMPS && !SHADE && !wide && dirs) {  // (narrow trees: below 2^28 nodes)
         if (seg) launch_dirs<AO, true>(dirs, grid, block, st, P);
         else launch_dirs<AO, false>(dirs, grid, block, st, P);
         return;
+    }
+    if (SHADE && !wide && dirs) {  // the sun's octant (shadow rays)
+        switch (dirs) {
+            case 1: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); return;
+            case 2: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); return;
+            case 3: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); return;
+            case 4: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); return;
+            case 5: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); return;
+            case 6: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); return;
+            case 7: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); return;
+            default: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); return;
+        }
     }
     if (SHADE || seg) {
         if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, 0, st, P);
@@ -1675,8 +1688,14 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
+    // shadow rays all step with the sun's signs (an exact zero component: generic flags)
+    int sun_dirs = (P.flags & SVO_CAST_NO_OCTANT) ? 0 : 1;
+    for (int k = 0; k < 3 && sun_dirs; k++) {
+        if (P.sun[k] < 0.0f) sun_dirs += 1 << k;
+        else if (!(P.sun[k] > 0.0f)) sun_dirs = 0;
+    }
     launch_cast<false, false, false, true>(wide_nodes(t, d->flags) || wide_nodes(sc, d->flags), true, dim3((uint32_t)blocks), dim3(kBlock),
-                                           (hipStream_t)stream, P);
+                                           (hipStream_t)stream, P, sun_dirs);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
