@@ -30,6 +30,15 @@ enum : int32_t { MODE_FRAME = 0, MODE_EXPLICIT = 1, MODE_SINGLE = 2 };
 
 constexpr int kMaxOrderRows = 512;   // local tile rows a dispatch order is kept for (4K: 270)
 
+// dda_axis for a ray from origin o along a direction whose step signs are known: cell = trunc(o)
+// and frac = exact - cell (exact = o, or o - 1 when the step is negative), both exact; a ray's
+// first crossing is then adelta - frac * delta (frac * delta exact in double: one rounding, as
+// dda_axis' product and difference)
+struct FrameAxes {
+    double frac[3];
+    int32_t cell[3];
+};
+
 struct CastParams {
     const Node* nodes;
     const uint16_t* mats;
@@ -48,6 +57,9 @@ struct CastParams {
     int32_t n_frames;        // frames in this launch (>= 1); frame f casts from frame_org[3f..]
     int64_t frame_records;   // records of one frame (this shard)
     float frame_org[3 * SVO_MAX_FRAMES];
+    // octant instances (frame_dirs): dda_axis' per-axis set-up of each frame origin, hoisted to the
+    // host (the same for every ray of the frame: the steps' signs are the octant's)
+    FrameAxes fax[SVO_MAX_FRAMES];
     int32_t use_row_order;                // dispatch order of the local tile rows (else top first)
     uint16_t row_order[kMaxOrderRows];
     // explicit mode
@@ -692,16 +704,31 @@ __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS =
 template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
-                                     Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1) {
+                                     Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1,
+                                     const FrameAxes* fx = nullptr) {
     Ray R;
+    if (DIRS != 0 && fx) {
+        // a frame ray of an octant instance: the origin's part of dda_axis is the frame's (fx)
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const Dda1 ax = dda_axis(o[k], d[k]);
-        R.r[k] = ax.cell;
-        R.T[k] = ax.dpos;
-        R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
-        R.s[k] = ax.step;
-        R.ia[k] = __builtin_amdgcn_rcpf((float)ax.adelta);
+        for (int k = 0; k < 3; k++) {
+            const float df = rcp_rn(d[k]);
+            const double delta = (double)df;
+            R.r[k] = fx->cell[k];
+            R.T[k] = __builtin_fma(-fx->frac[k], delta, __builtin_fabs(delta));
+            R.af[k] = __builtin_fabsf(df);
+            R.s[k] = dirs_sign(DIRS, k);
+            R.ia[k] = __builtin_amdgcn_rcpf(R.af[k]);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const Dda1 ax = dda_axis(o[k], d[k]);
+            R.r[k] = ax.cell;
+            R.T[k] = ax.dpos;
+            R.af[k] = (float)ax.adelta;  // exact: adelta is |f32 quotient|
+            R.s[k] = ax.step;
+            R.ia[k] = __builtin_amdgcn_rcpf((float)ax.adelta);
+        }
     }
     R.steps = budget;
     R.axis = 3u;
@@ -716,6 +743,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // non-linear: need_seg).  The other one runs exact-origin rays only; it re-tests them cheaply
     // (lin_origin) and steps any other ray voxel by voxel.
     bool lin = SEG ? fast && exact_axis(R.T[0], R.a(0), budget) && exact_axis(R.T[1], R.a(1), budget) && exact_axis(R.T[2], R.a(2), budget)
+                   : (DIRS != 0 && fx) ? fast  // (need_seg: this instance's frame origins are exact)
                    : ((unsigned)fast & (unsigned)lin_origin(o[0]) & (unsigned)lin_origin(o[1]) & (unsigned)lin_origin(o[2])) != 0u;
     if (!SEG) fast = lin;
     const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
@@ -1120,6 +1148,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
+    uint32_t frm = 0u;  // the wave's frame (frame mode)
     if (P.mode == MODE_FRAME) {
         // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes.
         // The tile index is wave-uniform: its division runs on the scalar unit.
@@ -1127,6 +1156,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         // indices are wave-uniform: their divisions run on the scalar unit
         const uint32_t wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
+        frm = fr;
         const int32_t lane = (int32_t)(threadIdx.x & 63u);
         const uint32_t tq = tile / (uint32_t)P.tiles_x;
         int32_t trl = (int32_t)tq;
@@ -1215,7 +1245,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
     } else if (out >= 0) {
         Parent pfin;
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
-                                   nullptr, AO ? &pfin : nullptr, -1, P.top_solid);
+                                   nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
         reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
         P.t[out] = h.t;
         P.info[out] = h.info;
@@ -1435,6 +1465,19 @@ static bool need_seg(const CastParams& P) {
     for (int32_t i = 0; i < 3 * nf; i++)
         if (!(2.0f * org[i] == __builtin_truncf(2.0f * org[i]) && __builtin_fabsf(org[i]) < 1073741824.0f)) return true;
     return false;
+}
+
+// the octant's frame set-up (FrameAxes) for every frame of the launch
+static void frame_axes(CastParams& P, int dirs) {
+    if (dirs == 0) return;
+    for (int32_t f = 0; f < P.n_frames; f++)
+        for (int k = 0; k < 3; k++) {
+            const float o = P.frame_org[3 * f + k];
+            const int32_t cell = (int32_t)__builtin_truncf(o);
+            const double exact = ((dirs - 1) >> k) & 1 ? (double)o - 1.0 : (double)o;
+            P.fax[f].cell[k] = cell;
+            P.fax[f].frac[k] = exact - (double)cell;
+        }
 }
 
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
@@ -1726,15 +1769,17 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     const dim3 grid((uint32_t)blocks), block(kBlock);
     hipStream_t st = (hipStream_t)stream;
     const bool wide = wide_nodes(t, d->flags), seg = need_seg(P);
+    const int dirs = frame_dirs(P);
+    frame_axes(P, dirs);
     if (P.ao_n > 0) {
         if (P.flags & SVO_CAST_STATS) launch_cast<true, true, true, false>(wide, seg, grid, block, st, P);
-        else launch_cast<false, false, true, false>(wide, seg, grid, block, st, P, frame_dirs(P));
+        else launch_cast<false, false, true, false>(wide, seg, grid, block, st, P, dirs);
     } else if (P.flags & SVO_CAST_STATS) {
         launch_cast<true, true, false, false>(wide, seg, grid, block, st, P);
     } else if (P.flags & SVO_CAST_TIMELINE) {
         launch_cast<false, true, false, false>(wide, seg, grid, block, st, P);
     } else {
-        launch_cast<false, false, false, false>(wide, seg, grid, block, st, P, frame_dirs(P));
+        launch_cast<false, false, false, false>(wide, seg, grid, block, st, P, dirs);
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
