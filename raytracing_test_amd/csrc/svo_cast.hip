@@ -498,9 +498,11 @@ struct WideNodes {
 
 // SPLIT: the levels above the bricks hold interior nodes or SOLID regions only; a SOLID region ends
 // the ray, so the parent may be overwritten by it, and those levels need no leaf branch and no
-// copies of the loaded node (instances whose callers read the final parent — AO's brick_near, the
-// shading pass's uniform regions — keep the general loop)
-template <bool STATS, bool SPLIT, class Mem>
+// copies of the loaded node (the shading pass, whose callers read the final parent's regions, keeps
+// the general loop).  PSH (AO instances: ao_count_plan reads the final parent's shift only): a SOLID
+// region above the bricks leaves the shift of its own parent, so no path entry at or below the
+// SOLID node is read back
+template <bool STATS, bool SPLIT, bool PSH, class Mem>
 __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, const Path& path,
                                            const uint32_t w[3], uint32_t moved, Parent& par, uint32_t& sh_out, uint64_t& bmask,
                                            uint32_t& bref, uint32_t& binfo, Stats& st) {
@@ -546,11 +548,11 @@ __device__ __forceinline__ uint32_t lookup(const CastParams& P, const Mem& mem, 
             path.put(dd, n.mask, n.ref);
             par.mask = n.mask;
             par.ref = n.ref;
-            par.sh = sh;
             binfo = n.info;
             const uint64_t t = slot_top(n.mask, child_slot(w[0], w[1], w[2], sh));
             const bool occ = (int64_t)t < 0;
             const bool solid = (n.info & K_KIND_MASK) == K_SOLID;
+            par.sh = PSH && solid ? sh + 2u : sh;
             ni = popc_add(t, n.ref);
             dd++;
             pend = occ && !solid;
@@ -692,7 +694,8 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 }
 
 // par_out: receives the parent of the region the ray ended in (it holds the final voxel; the LDS
-// path holds its ancestors at depths 0 .. levels-1-sh/2)
+// path holds its ancestors at depths 0 .. levels-1-sh/2).  KEEPPAR (AO): only its shift is exact
+// (lookup: PSH) — a ray ending in a SOLID region above the bricks leaves that region's mask and ref
 // ESCAPE (shading rays whose end position is not output): a ray moving up above the highest stored
 // voxel row `top` (wrapped) whose budget cannot carry it past the extent in y leaves the loop as a
 // miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off).
@@ -803,7 +806,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
-        const uint32_t kind = lookup<STATS, !REFLECT && !KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
+        const uint32_t kind = lookup<STATS, !REFLECT, KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
