@@ -155,6 +155,7 @@ struct Ray {
     uint32_t axis;  // axis of the last step (3: none)
     float tlast;    // crossing value of the last step, as output (f32)
     float ia[3];    // f32 estimate of 1/absDelta (crossing counts only estimate with it)
+    int32_t rb[3];  // segment-cached instances (skip_box RB): the cell of each axis' last exact crossing
     __device__ __forceinline__ float inv_a(int k) const { return ia[k]; }
     __device__ __forceinline__ double a(int k) const { return (double)af[k]; }
 };
@@ -349,13 +350,33 @@ __device__ __forceinline__ int32_t seg_cap(double T, float af, float inva) {
 // the wave holds rays that are not linear): each axis' exit event is also held to its exact segment (seg_cap); an exit on such a
 // bound is a virtual one inside the box (the next lookup finds the same empty cell in the parent's
 // mask, without a load, and the crossing continues).
-template <bool TRACK = true>
+// RB: segment bounds cached as cells (R.rb): crossing i of axis k from the current state is the one
+// into cell r + s*i, so the bound seg_cap gave at some earlier state stays s*(rb - r) crossings ahead
+// while the ray has not passed it (every sum up to there is exact, from any state on the way); a
+// negative count means it has, and seg_cap is taken again from the current state
+template <bool TRACK = true, bool RB = false>
 __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) {
     // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) e[k] = min(ex[k], R.steps);
-    if (seg) {  // wave-uniform
+    if (seg && RB) {  // wave-uniform
+        int32_t cap[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++)  // (wrapping differences: |cap| < 2^31)
+            cap[k] = (int32_t)(R.s[k] > 0 ? (uint32_t)R.rb[k] - (uint32_t)R.r[k] : (uint32_t)R.r[k] - (uint32_t)R.rb[k]);
+        if (__ballot(min(min(cap[0], cap[1]), cap[2]) < 0) != 0ull) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                if (cap[k] < 0) {
+                    cap[k] = seg_cap(R.T[k], R.af[k], R.inv_a(k));
+                    R.rb[k] = (int32_t)(R.s[k] > 0 ? (uint32_t)R.r[k] + (uint32_t)cap[k] : (uint32_t)R.r[k] - (uint32_t)cap[k]);
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) e[k] = min(e[k], cap[k]);
+    } else if (seg) {  // wave-uniform
 #pragma unroll
         for (int k = 0; k < 3; k++) e[k] = min(e[k], seg_cap(R.T[k], R.af[k], R.inv_a(k)));
     }
@@ -750,6 +771,12 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                    : ((unsigned)fast & (unsigned)lin_origin(o[0]) & (unsigned)lin_origin(o[1]) & (unsigned)lin_origin(o[2])) != 0u;
     if (!SEG) fast = lin;
     const bool wseg = SEG && __ballot(fast && !lin) != 0ull;  // wave-uniform (REFLECT: taken per crossing)
+    // octant segment instances cache their segment bounds (skip_box RB); none yet (cap -1)
+    constexpr bool RB = SEG && DIRS != 0 && !REFLECT;
+    if (RB) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) R.rb[k] = R.r[k] - R.s[k];
+    }
     // Instances without segments run rays from integral / half-integral origins only (need_seg):
     // every sum they take is exact, so they recover the output crossing value once at the end
     // (T - a on the last step's axis) instead of keeping it on every brick step
@@ -784,7 +811,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         wrap3(R, wm, w);
         if ((int32_t)w[1] > pre_top) {
             const int32_t ex[3] = {R.steps, R.s[1] < 0 ? (int32_t)w[1] - pre_top - 1 : (int32_t)(wm - w[1]), R.steps};
-            skip_box<TRACK>(R, ex, wseg);
+            skip_box<TRACK, RB>(R, ex, wseg);
         }
     }
     // one back-edge: every path through the body ends at the loop latch
@@ -819,7 +846,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
                        box_exits(w, R.s, sh, par.mask, ud, ex);
-                       return skip_box<TRACK>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
+                       return skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                    }())) {
             if (STATS && fast) st.skip_out++;
             if (fast) {

@@ -449,6 +449,32 @@ def test_ao_reference_world(rt, gtree, ref_world_oracle, n_ao):
             assert out["ao"].max() <= n_ao
 
 
+def test_ao_upper_level_solids(rt, oracle_mod, torch_cuda):
+    """AO on hits inside SOLID regions above the brick level (16^3 blocks put at level 4, floating
+    in the camera's view): the AO primaries' split lookup leaves the region's parent shift for the
+    plan (lookup: PSH); counts against the oracle for the plan, its octant-free form and traced rays."""
+    corners = [(64, 48, 64), (112, 48, 96), (80, 64, 80), (96, 32, 48), (48, 64, 112)]
+    w = rt.World.reference()
+    o = oracle_mod.Tree.reference_world()
+    for i, (x, y, z) in enumerate(corners):
+        w.put_block(x, y, z, 0, 1000 + i, level=4)
+        assert o.put_block(x, y, z, 0, 1000 + i, 0.0, 4) == 0
+    gt = w.build().upload(0)
+    for org, d in CAMERAS[:2]:
+        dn = rt.normalize(d)
+        ao, hit = o.cast_frame_ao(org, dn, 128, 96, 300, 16, 5)
+        for flags in (0, rt.CAST_NO_OCTANT, rt.CAST_AO_TRACE):
+            out = rt.decode_hits(gt.cast_frame(org, dn, 128, 96, 300, ao_samples=16, ao_steps=5, flags=flags))
+            assert np.array_equal(out["hit"], hit != 0)
+            assert np.array_equal(out["ao"], ao), (org, flags)
+        # the blocks are hit (their faces, not only bricks around them)
+        pos = out["pos"][out["hit"]]
+        inb = np.zeros(len(pos), bool)
+        for c in corners:
+            inb |= np.all((pos >= np.array(c)) & (pos < np.array(c) + 16), axis=1)
+        assert inb.sum() > 200, (org, inb.sum())
+
+
 @pytest.mark.parametrize("n_ao,ao_steps", [(1, 5), (16, 0), (16, 1), (20, 12), (64, 3), (7, 40)])
 def test_ao_plan_budgets(rt, gtree, ref_world_oracle, n_ao, ao_steps):
     """The AO plan over sample counts and budgets (1 .. 64 samples, 0 .. 40 steps) against the oracle."""
