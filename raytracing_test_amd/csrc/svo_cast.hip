@@ -302,9 +302,13 @@ __device__ __forceinline__ int32_t add_bit(int32_t x, uint64_t m) {
     asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(co) : "v"(x), "s"(m));
     return r;
 }
-__device__ __forceinline__ int32_t count_est(double T, double a, float inva, double V, double& E) {
+// The difference V - T is taken in f32 from f32 copies of both (one conversion of V serves the three
+// axes): T / a and V / a stay below budget + 2 < 2^20 + 2 (V is at most T + steps * a on every axis),
+// so the two conversions, the subtraction, the 1-ulp reciprocal and the fma move the estimate by less
+// than 6 * 2^20 * 2^-24 = 3/8 < 1/2 — m stays c - 1 or c
+__device__ __forceinline__ int32_t count_est(double T, double a, float inva, double V, float Vf, double& E) {
     uint32_t mu;
-    asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf((float)(V - T), inva, 0.5f)));
+    asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf(Vf - (float)T, inva, 0.5f)));
     E = on_grid(T, (int32_t)mu, a);
     return (int32_t)mu;
 }
@@ -396,9 +400,10 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
     // itself, so x and y need no second compare of their own for it.
     int32_t n[3];
     double F[3];
-    n[0] = count_est(R.T[0], R.a(0), R.inv_a(0), V, F[0]);
-    n[1] = count_est(R.T[1], R.a(1), R.inv_a(1), V, F[1]);
-    n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, F[2]);
+    const float Vf = (float)V;
+    n[0] = count_est(R.T[0], R.a(0), R.inv_a(0), V, Vf, F[0]);
+    n[1] = count_est(R.T[1], R.a(1), R.inv_a(1), V, Vf, F[1]);
+    n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, Vf, F[2]);
     // (the terms of one axis are disjoint: a tie term implies F = V)
     n[0] = add_bit(n[0], __ballot(F[0] < V) | mx);
     n[1] = add_bit(n[1], __ballot(F[1] < V) | my | (mx & __ballot(F[1] == V)));

@@ -69,3 +69,39 @@ def test_segment_cap_is_exact():
                 assert _closed(i, a, T) == t, (o, d, c, i)
                 checked += 1
     assert checked > 10000
+
+
+def _count_est(T, af, inva, V):
+    # svo_cast.hip count_est: m = cvt_u32(fma_f32(f32(V) - f32(T), inva, 0.5)) (the f32 fma emulated
+    # as the exact product plus 1/2 in double, rounded to f32 once more; v_cvt_u32_f32 truncates and
+    # saturates at 0)
+    x = np.float32(np.float32(V) - np.float32(T))
+    y = np.float32(float(x) * float(np.float32(inva)) + 0.5)
+    return int(max(np.trunc(float(y)), 0.0))
+
+
+def test_count_estimate_within_one():
+    """skip_box's crossing counts start from an f32 estimate m of #{j >= 0 : T + j*a < V} (or <=):
+    m must be the count c or c - 1 (one exact f64 test then settles it).  States as the kernel reaches
+    them: T a crossing value of an axis after up to 2^20 crossings, V any value up to T + steps * a
+    (budget < 2^20 in all), the reciprocal off by up to 1 ulp (v_rcp_f32)."""
+    rng = np.random.default_rng(11)
+    for _ in range(20000):
+        a = float(np.float32(2.0 ** rng.uniform(-2, 12)))
+        af = np.float32(a)
+        inva = np.float32(1.0) / af
+        inva = np.nextafter(inva, np.float32(rng.choice([0.0, np.inf]))) if rng.random() < 0.5 else inva
+        budget = int(rng.choice([300, 16384, (1 << 20) - 1]))
+        j = int(rng.integers(0, budget))
+        T = float(Fraction(a) * (j + 1) - Fraction(a) * Fraction(float(np.float32(rng.random()))))
+        steps = budget - j
+        V = T + float(rng.random()) * steps * a
+        if rng.random() < 0.3:  # V on a crossing of this axis, or next to one
+            i = int(rng.integers(0, steps + 1))
+            V = float(np.nextafter(_closed(i, a, T), rng.choice([-np.inf, np.inf]))) if rng.random() < 0.5 else _closed(i, a, T)
+        m = _count_est(T, af, inva, V)
+        xs = (Fraction(V) - Fraction(T)) / Fraction(a)
+        c_lt = max(0, -(-xs.numerator // xs.denominator))  # #{j >= 0 : T + j a < V} = ceil(x)
+        c_le = max(0, xs.numerator // xs.denominator + 1)  # #{j >= 0 : T + j a <= V} = floor(x) + 1
+        assert m in (c_lt - 1, c_lt) or c_lt == 0 and m == 0, (T, a, V, m, c_lt)
+        assert m in (c_le - 1, c_le) or c_le == 0 and m == 0, (T, a, V, m, c_le)
