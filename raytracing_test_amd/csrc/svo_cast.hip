@@ -165,6 +165,14 @@ __device__ __forceinline__ double on_grid(double T, int32_t k, double a) {
     return __builtin_fma((double)k, a, T);
 }
 
+// The f32 count estimates (count_est) need every exit event V in f32 range: V is at most the
+// smallest absDelta times budget + 2 (< 2^21), so a ray whose every absDelta is 2^100 or more (a
+// direction vector with every component below 2^-100) takes the stepping path.  (Frame rays have unit
+// directions: their smallest absDelta is at most sqrt(3).)
+__device__ __forceinline__ bool span_ok(const Ray& R) {
+    return __builtin_fminf(__builtin_fminf(R.af[0], R.af[1]), R.af[2]) < 0x1p100f;
+}
+
 // one DDA step (ray_caster.cpp:70-80), branch-free
 __device__ __forceinline__ void dda_step(Ray& R) {
     const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
@@ -303,9 +311,20 @@ __device__ __forceinline__ int32_t add_bit(int32_t x, uint64_t m) {
     return r;
 }
 // The difference V - T is taken in f32 from f32 copies of both (one conversion of V serves the three
-// axes): T / a and V / a stay below budget + 2 < 2^20 + 2 (V is at most T + steps * a on every axis),
+// axes; V < 2^121 by span_ok, so its copy is finite, and a T beyond the f32 range only makes the
+// estimate 0, its count): T / a and V / a stay below budget + 2 < 2^20 + 2 (V is at most T + steps * a on every axis),
 // so the two conversions, the subtraction, the 1-ulp reciprocal and the fma move the estimate by less
 // than 6 * 2^20 * 2^-24 = 3/8 < 1/2 — m stays c - 1 or c
+// V, or nextup(V) on the lanes of m (V >= 0 and finite: the bits plus one)
+__device__ __forceinline__ double next_if(double V, uint64_t m) {
+    const uint64_t b = (uint64_t)__double_as_longlong(V);
+    uint32_t lo, hi;
+    uint64_t c, c2;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(lo), "=s"(c) : "v"((uint32_t)b), "s"(m));
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(hi), "=s"(c2) : "v"((uint32_t)(b >> 32)), "s"(c));
+    (void)c2;
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ int32_t count_est(double T, double a, float inva, double V, float Vf, double& E) {
     uint32_t mu;
     asm("v_cvt_u32_f32 %0, %1" : "=v"(mu) : "v"(__builtin_fmaf(Vf - (float)T, inva, 0.5f)));
@@ -406,7 +425,9 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
     n[2] = count_est(R.T[2], R.a(2), R.inv_a(2), V, Vf, F[2]);
     // (the terms of one axis are disjoint: a tie term implies F = V)
     n[0] = add_bit(n[0], __ballot(F[0] < V) | mx);
-    n[1] = add_bit(n[1], __ballot(F[1] < V) | my | (mx & __ballot(F[1] == V)));
+    // y's tie term: exit on x counts y's events <= V, i.e. < nextup(V) (V >= 0 finite: its bits + 1),
+    // taken by one integer add with the carry-in on mx instead of a second f64 compare
+    n[1] = add_bit(n[1], __ballot(F[1] < next_if(V, mx)) | my);
     n[2] = add_bit(n[2], __ballot(F[2] <= V));
     const int32_t total = n[0] + n[1] + n[2];
     if (total > R.steps) return false;
@@ -767,7 +788,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // takes the cheaper crossing
     // (bitwise ands: one straight-line computation, no branch per term)
     bool fast = ((unsigned)!(P.flags & SVO_CAST_ITERATIVE) & (unsigned)(budget < (1 << 20)) & (unsigned)axis_ok(R.T[0], R.a(0)) &
-                 (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2))) != 0u;
+                 (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2)) & (unsigned)((DIRS != 0 && fx) || span_ok(R))) != 0u;  // (frame rays: unit directions)
     // SEG: the instance carries segment-bounded crossings (the host picks it when rays can be
     // non-linear: need_seg).  The other one runs exact-origin rays only; it re-tests them cheaply
     // (lin_origin) and steps any other ray voxel by voxel.
@@ -957,7 +978,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                     R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
                 }
                 fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
-                       axis_ok(R.T[2], R.a(2));
+                       axis_ok(R.T[2], R.a(2)) && span_ok(R);
                 lin = fast && exact_axis(R.T[0], R.a(0), R.steps) && exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
                 if (!SEG) fast = lin;  // (REFLECT runs in SEG instances)
             }

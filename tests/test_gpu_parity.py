@@ -41,7 +41,8 @@ def compare(rt, tree, gpu_out, ref, label):
     assert np.array_equal(g["last_pos"], ref["last"]), label
     mid = np.where(g["hit"], g["material"], 0)
     assert np.array_equal(pf[mid], ref["flags"]) and np.array_equal(pc[mid], ref["color"]), label
-    rt_ = ref["t"].astype(np.float32)
+    with np.errstate(over="ignore"):  # (crossing values beyond the f32 range are inf on both sides)
+        rt_ = ref["t"].astype(np.float32)
     gt = g["t"]
     fin = np.isfinite(rt_)
     assert np.array_equal(np.isnan(gt), np.isnan(rt_)), label
@@ -135,6 +136,30 @@ def test_edge_case_rays(rt, oracle_mod, torch_cuda, gtree, ref_world_oracle):
         for flags in (0, rt.CAST_ITERATIVE, rt.CAST_WIDE_ADDR):
             out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins[sel], dirs[sel], steps, flags)
             compare(rt, gtree, out, ref, "edge S=%d flags=%d" % (steps, flags))
+
+
+def test_tiny_direction_rays(rt, torch_cuda, gtree, ref_world_oracle):
+    """Unnormalised directions with tiny components (absDelta up to ~1e37): crossing values far above
+    the f32 range.  castRayFromCam's double DDA walks them like the unit directions they scale; the
+    kernel's closed-form crossings estimate counts in f32, so rays whose every absDelta is >= 2^100
+    take the stepping path (span_ok), the others cross boxes as usual."""
+    n = rt.normalize
+    base = [((5.5, 200.0, 5.5), n([0.3, -1, 0.2])), ((40.0, 90.0, 40.0), n([1, -0.45, 1])),
+            ((120.25, 70.5, 30.75), n([-0.6, -0.5, 0.4])), ((60.0, 61.0, 60.0), n([0.01, -1, 0.02]))]
+    origins, dirs = [], []
+    for o, d in base:
+        # (8e-38: every absDelta above 2^100 and every box exit event beyond the f32 range; the 0.01
+        # component becomes subnormal there, an infinite absDelta)
+        for scale in (1.0, 3e-20, 1.7e-30, 1e-34, 8e-38):
+            origins.append(o)
+            dirs.append([np.float32(c * scale) for c in d])
+    origins = np.array(origins, np.float32)
+    dirs = np.array(dirs, np.float32)
+    for steps in (300, 3000):
+        for flags in (0, rt.CAST_ITERATIVE):
+            out, ref = _explicit(rt, torch_cuda, gtree, ref_world_oracle, origins, dirs, steps, flags)
+            compare(rt, gtree, out, ref, "tiny dirs S=%d flags=%d" % (steps, flags))
+            assert ref["hit"].sum() >= len(base) * 3  # they reach the terrain
 
 
 def _segment_hits_box(o, d, tmax, lo, hi):
