@@ -783,12 +783,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     R.steps = budget;
     R.axis = 3u;
     R.tlast = 0.0f;
-    // closed-form crossings (fast): budget < 2^20 also keeps the f32 count estimates within 1/4 of
+    // closed-form crossings (fast): budget < 2^20 also keeps the f32 count estimates within 3/8 of
     // the truth (count_est, seg_cap); linear rays need no segment bounds, and a wave of linear rays
-    // takes the cheaper crossing
+    // takes the cheaper crossing.  Origins within 2^30 (an exact start cell: deltaPos starts in
+    // [0, 2 absDelta]); beyond them castRayFromCam's int conversion is undefined, and those rays step
+    // voxel by voxel (no closed form over a start cell the conversion clamped)
     // (bitwise ands: one straight-line computation, no branch per term)
     bool fast = ((unsigned)!(P.flags & SVO_CAST_ITERATIVE) & (unsigned)(budget < (1 << 20)) & (unsigned)axis_ok(R.T[0], R.a(0)) &
-                 (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2)) & (unsigned)((DIRS != 0 && fx) || span_ok(R))) != 0u;  // (frame rays: unit directions)
+                 (unsigned)axis_ok(R.T[1], R.a(1)) & (unsigned)axis_ok(R.T[2], R.a(2)) & (unsigned)((DIRS != 0 && fx) || span_ok(R)) &  // (frame rays: unit directions)
+                 (unsigned)(!SEG || (__builtin_fabsf(o[0]) < 0x1p30f && __builtin_fabsf(o[1]) < 0x1p30f &&
+                                     __builtin_fabsf(o[2]) < 0x1p30f))) != 0u;  // (!SEG: need_seg bounds the origins)
     // SEG: the instance carries segment-bounded crossings (the host picks it when rays can be
     // non-linear: need_seg).  The other one runs exact-origin rays only; it re-tests them cheaply
     // (lin_origin) and steps any other ray voxel by voxel.
@@ -977,7 +981,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                     R.af[k] = (float)ad;
                     R.ia[k] = __builtin_amdgcn_rcpf((float)ad);
                 }
-                fast = !(P.flags & SVO_CAST_ITERATIVE) && R.steps < (1 << 20) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
+                // (deltaPos restarts from the shader's origin, not the current cell: |T| / absDelta
+                // is bounded by the distance travelled, so the initial budget is held below 2^19 to
+                // keep the count estimates within 1/2 — count_est)
+                fast = !(P.flags & SVO_CAST_ITERATIVE) && budget < (1 << 19) && axis_ok(R.T[0], R.a(0)) && axis_ok(R.T[1], R.a(1)) &&
                        axis_ok(R.T[2], R.a(2)) && span_ok(R);
                 lin = fast && exact_axis(R.T[0], R.a(0), R.steps) && exact_axis(R.T[1], R.a(1), R.steps) && exact_axis(R.T[2], R.a(2), R.steps);
                 if (!SEG) fast = lin;  // (REFLECT runs in SEG instances)

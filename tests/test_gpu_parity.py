@@ -162,6 +162,25 @@ def test_tiny_direction_rays(rt, torch_cuda, gtree, ref_world_oracle):
             assert ref["hit"].sum() >= len(base) * 3  # they reach the terrain
 
 
+def test_huge_origin_rays_terminate(rt, torch_cuda, gtree):
+    """Origins beyond the int range (castRayFromCam's `(int)` of them is undefined behaviour, so there is
+    no reference result): the launch must end, and the closed-form path must agree with voxel stepping
+    (both start from the same clamped cell)."""
+    rng = np.random.default_rng(5)
+    vals = [1e10, -3e9, 2147483648.0, -2147483904.0, 1.5e30, -3.4e38, 1073741824.0, 1073741760.5]
+    org = np.array([[rng.choice(vals), rng.uniform(0, 120), rng.uniform(0, 200)] for _ in range(64)], np.float32)
+    org[::2] = org[::2][:, [1, 0, 2]]
+    org[::3] = org[::3][:, [2, 1, 0]]
+    d = rng.normal(size=(64, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    gd, go = torch_cuda.from_numpy(d).cuda(), torch_cuda.from_numpy(org).cuda()
+    for steps in (300, 5000):
+        a = rt.decode_hits(gtree.cast_rays(gd, go, steps=steps))
+        b = rt.decode_hits(gtree.cast_rays(gd, go, steps=steps, flags=rt.CAST_ITERATIVE))
+        for k in ("pos", "hit", "steps", "last_pos"):
+            assert np.array_equal(a[k], b[k]), (steps, k)
+
+
 def _segment_hits_box(o, d, tmax, lo, hi):
     """slab test of segments o + t d, t in [0, tmax], against the box [lo, hi] (conservative)"""
     with np.errstate(divide="ignore", invalid="ignore"):
