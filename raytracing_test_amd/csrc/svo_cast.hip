@@ -153,7 +153,7 @@ struct Ray {
     int32_t s[3];   // step
     int32_t steps;  // budget left
     uint32_t axis;  // axis of the last step (3: none)
-    float tlast;    // crossing value of the last step, as output (f32)
+    double tlast;   // crossing value of the last step (converted to the f32 output once, at the end)
     float ia[3];    // f32 estimate of 1/absDelta (crossing counts only estimate with it)
     int32_t rb[3];  // segment-cached instances (skip_box RB): the cell of each axis' last exact crossing
     __device__ __forceinline__ float inv_a(int k) const { return ia[k]; }
@@ -178,7 +178,7 @@ __device__ __forceinline__ void dda_step(Ray& R) {
     const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
     const bool cy = !cx && (R.T[1] < R.T[2]);
     const bool cz = !cx && !cy;
-    R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+    R.tlast = cx ? R.T[0] : (cy ? R.T[1] : R.T[2]);
     R.axis = cx ? 0u : (cy ? 1u : 2u);
     R.r[0] += cx ? R.s[0] : 0;
     R.r[1] += cy ? R.s[1] : 0;
@@ -438,7 +438,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
         // (full rate; s = +-1, |n| < 2^21)
         R.r[k] += __builtin_constant_p(R.s[k]) ? (R.s[k] > 0 ? n[k] : -n[k]) : __mul24(R.s[k], n[k]);
     }
-    if (TRACK) R.tlast = (float)V;  // (else recovered at the end of the ray: trace)
+    if (TRACK) R.tlast = V;  // (else recovered at the end of the ray: trace)
     R.axis = sel32(mx, 0u, sel32(my, 1u, 2u));
     R.steps -= total;
     return true;
@@ -694,7 +694,7 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
             // one DDA step (ray_caster.cpp:70-80) without position updates
             const bool cx = (R.T[0] < R.T[1]) && (R.T[0] < R.T[2]);
             const bool cy = !cx && (R.T[1] < R.T[2]);
-            if (TRACK) R.tlast = (float)(cx ? R.T[0] : (cy ? R.T[1] : R.T[2]));
+            if (TRACK) R.tlast = cx ? R.T[0] : (cy ? R.T[1] : R.T[2]);
             R.T[0] = cx ? R.T[0] + R.a(0) : R.T[0];
             R.T[1] = cy ? R.T[1] + R.a(1) : R.T[1];
             R.T[2] = (cx || cy) ? R.T[2] : R.T[2] + R.a(2);  // (a mask or, not a fourth f64 compare)
@@ -782,7 +782,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     }
     R.steps = budget;
     R.axis = 3u;
-    R.tlast = 0.0f;
+    R.tlast = 0.0;
     // closed-form crossings (fast): budget < 2^20 also keeps the f32 count estimates within 3/8 of
     // the truth (count_est, seg_cap); linear rays need no segment bounds, and a wave of linear rays
     // takes the cheaper crossing.  Origins within 2^30 (an exact start cell: deltaPos starts in
@@ -1056,14 +1056,14 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         // with an infinite crossing (deltaPos = inf - frac * inf), which stays inf
         const double Ta = R.axis == 0u ? R.T[0] : (R.axis == 1u ? R.T[1] : R.T[2]);
         const float aa = R.axis == 0u ? R.af[0] : (R.axis == 1u ? R.af[1] : R.af[2]);
-        R.tlast = (float)(__builtin_isinf(aa) ? Ta : Ta - (double)aa);
+        R.tlast = __builtin_isinf(aa) ? Ta : Ta - (double)aa;
     }
     Hit h;
     h.x = R.r[0];
     h.y = R.r[1];
     h.z = R.r[2];
     h.steps_left = hit ? R.steps : 0;
-    h.t = R.tlast;
+    h.t = (float)R.tlast;  // (one rounding of the same double as before)
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
     h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (hit ? mat & MAT_MASK : 0u);
