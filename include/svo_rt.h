@@ -203,10 +203,12 @@ typedef struct {
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
                           lane work units, wave-max work units x 64, crossings by box cell
                           size (4 slots), brick visits, wave-level loop iterations,
-                          wave-level brick voxel steps, (reserved), lookups started at
+                          wave-level brick voxel steps, loop iterations that left a ray
+                          more budget than they found (0 by construction), lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
-                          per-lane path; then 2 stamps per block (svo_cast_blocks);
+                          per-lane path, node loads of the AO plan's brick lookups;
+                          then 2 stamps per block (svo_cast_blocks);
                           then, with SVO_CAST_STATS in frame mode, one word per
                           output pixel: lookups | brick steps << 32
                           (SVO_CAST_STATS or SVO_CAST_TIMELINE) */
@@ -232,8 +234,8 @@ typedef struct {
    stats must hold SVO_STATS_HEADER + 2 * svo_cast_blocks() [+ pixels with SVO_CAST_STATS] words */
 #define SVO_STATS_HEADER 32
 #define SVO_CAST_TIMELINE 32
-/* svo_cast_desc.flags: map blocks to XCDs in contiguous frame bands */
-#define SVO_CAST_XCD_SWIZZLE 16
+/* (bits 16 and 1024 were round-2 dispatch experiments, XCD-contiguous bands and horizon-first row order:
+   measured slower or equal, removed) */
 /* svo_cast_desc.flags, AO (results identical): trace every AO ray through the tree instead of the
    per-face voxel plan (A/B reference path) */
 #define SVO_CAST_AO_TRACE 128
@@ -241,9 +243,6 @@ typedef struct {
    covers 16x4 pixels of its 8-pixel tile row; these bits select 8x8 or 32x2 instead */
 #define SVO_CAST_TILE_8X8 256
 #define SVO_CAST_TILE_32X2 512
-/* svo_cast_desc.flags, scheduling (results identical): dispatch tile rows in order of the vertical
-   slope of their centre ray, shallowest first (grazing rays travel furthest over terrain) */
-#define SVO_CAST_HORIZON_FIRST 1024
 /* svo_cast_desc.flags (results identical): read nodes through 64-bit addresses even when the tree is
    small enough for 32-bit buffer offsets (trees of more than 2^28 nodes always use them) */
 #define SVO_CAST_WIDE_ADDR 2048

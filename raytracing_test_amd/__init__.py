@@ -34,20 +34,18 @@ NONE, REFLECTIVE, REFRACTIVE, LUMINESCENT, LIQUID = 0x0, 0x2, 0x4, 0x8, 0x10
 CAST_ITERATIVE = 1  # svo_cast_desc.flags: voxel-by-voxel stepping (A/B reference path)
 CAST_STATS = 2  # svo_cast_desc.flags: accumulate traversal counters into desc.stats
 CAST_BOTTOM_FIRST = 4  # scheduling: bottom tile rows first (default is top first)
-CAST_XCD_SWIZZLE = 16  # contiguous frame band per XCD
 CAST_TIMELINE = 32  # per-block start/end stamps only
 CAST_AO_TRACE = 128  # AO: trace every AO ray instead of the per-face voxel plan (A/B reference)
 CAST_TILE_8X8 = 256  # scheduling: one wavefront per 8x8 tile (default: 16x4 pixels of its 8-pixel tile row)
 CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel tile row
-CAST_HORIZON_FIRST = 1024  # scheduling: tile rows with the shallowest centre ray first
 CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (results identical)
 CAST_SEGMENTS = 4096  # force the kernel instance with segment-exact crossings (results identical)
 CAST_NO_OCTANT = 16384  # per-wave step-sign flags instead of the launch's compiled-in sign octant (results identical)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
-              "reserved16", "root_starts", "cache_empty", "wave_skips", "wave_descents",
-              "path_starts")  # wave_*: per wave (64 rays)
+              "budget_grew", "root_starts", "cache_empty", "wave_skips", "wave_descents",
+              "path_starts", "ao_node_loads")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: one hit record in the exchange format (svo_hits_pack)

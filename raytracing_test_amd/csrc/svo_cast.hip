@@ -28,8 +28,6 @@ namespace {
 
 enum : int32_t { MODE_FRAME = 0, MODE_EXPLICIT = 1, MODE_SINGLE = 2 };
 
-constexpr int kMaxOrderRows = 512;   // local tile rows a dispatch order is kept for (4K: 270)
-
 // dda_axis for a ray from origin o along a direction whose step signs are known: cell = trunc(o)
 // and frac = exact - cell (exact = o, or o - 1 when the step is negative), both exact; a ray's
 // first crossing is then adelta - frac * delta (frac * delta exact in double: one rounding, as
@@ -60,8 +58,6 @@ struct CastParams {
     // octant instances (frame_dirs): dda_axis' per-axis set-up of each frame origin, hoisted to the
     // host (the same for every ray of the frame: the steps' signs are the octant's)
     FrameAxes fax[SVO_MAX_FRAMES];
-    int32_t use_row_order;                // dispatch order of the local tile rows (else top first)
-    uint16_t row_order[kMaxOrderRows];
     // explicit mode
     const float* rdir;
     const float* rorg;
@@ -332,6 +328,9 @@ __device__ __forceinline__ int32_t count_est(double T, double a, float inva, dou
     return (int32_t)mu;
 }
 
+// (v_max3_u32)
+__device__ __forceinline__ uint32_t max3u(uint32_t a, uint32_t b, uint32_t c) { return max(a, max(b, c)); }
+
 // Exact segments.  From any state (T, a), the crossings T + i*a are multiples of 2^v, v = the lower
 // of the lowest set bits of T and a, so every crossing below B = 2^(v+53) is exact and representable,
 // and the first one at or above B is that sum rounded once, as fma(i, a, T) computes it too.  B is at
@@ -430,7 +429,12 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
     n[1] = add_bit(n[1], __ballot(F[1] < next_if(V, mx)) | my);
     n[2] = add_bit(n[2], __ballot(F[2] <= V));
     const int32_t total = n[0] + n[1] + n[2];
-    if (total > R.steps) return false;
+    // Budget guard by construction: every count is at most its axis' clamped exit e[k] + 1 <= steps + 1
+    // (and the steps are below 2^20 on this path), so the move is taken only when each count, and the
+    // total, fits the steps left as unsigned values.  A count estimate gone wrong (saturated, or wrapped
+    // to a negative value, as before commit 1a85dd6) then ends the crossing here — the lanes take their
+    // last steps after the traversal loop — instead of growing the budget and never ending the launch.
+    if (max((uint32_t)total, max3u((uint32_t)n[0], (uint32_t)n[1], (uint32_t)n[2])) > (uint32_t)R.steps) return false;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
@@ -454,6 +458,7 @@ struct Stats {
                                         // parent mask
     uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
+    uint32_t budget_up;                            // loop iterations that left more budget than they found
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -824,7 +829,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -851,6 +856,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     while (!done) {
         // the voxel just entered is untested
         if (STATS) st.wv_iters += wave_lead();
+        const int32_t steps_in = R.steps;  // (STATS: the budget never grows)
         uint32_t w[3];
         wrap3(R, wm, w);
         if (ESCAPE && top >= 0 && R.s[1] > 0 && (int32_t)w[1] > top && (int64_t)w[1] + R.steps <= (int64_t)wm) {
@@ -1013,6 +1019,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 }
             }
         }
+        if (STATS && R.steps > steps_in) st.budget_up++;
     }
     const bool hit = mat != kNoHit;
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
@@ -1049,6 +1056,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
+        if (st.budget_up) atomicAdd(P.stats + 16, (unsigned long long)st.budget_up);
         if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
     }
     if (!TRACK && R.axis < 3u) {
@@ -1119,7 +1127,7 @@ __device__ __forceinline__ float3 sky_color(const float d[3], const float sun[3]
 // bricks: 0 or ~0)
 template <class Mem>
 __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& mem, const Path& path, const uint32_t w[3],
-                                               const uint32_t hw[3], int32_t dmax) {
+                                               const uint32_t hw[3], int32_t dmax, uint32_t& loads) {
     const uint32_t diff = ((w[0] ^ hw[0]) | (w[1] ^ hw[1]) | (w[2] ^ hw[2])) | 1u;
     const int32_t da = min(P.levels - 1 - (int32_t)((31u - (uint32_t)__builtin_clz(diff)) >> 1), dmax);  // (diff != 0)
     uint64_t mask = path.mask(da);
@@ -1132,6 +1140,7 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& m
         const uint64_t t = slot_top(mask, child_slot(w[0], w[1], w[2], sh));
         if ((int64_t)t < 0) {
             const Node n = mem.load(popc_add(t, ref));
+            loads++;
             const uint32_t kind = n.info & K_KIND_MASK;
             if (kind == K_INTERIOR) {
                 mask = n.mask;
@@ -1146,9 +1155,11 @@ __device__ __forceinline__ uint64_t brick_near(const CastParams& P, const Mem& m
     return res;
 }
 
+// loads: node loads of the plan's brick lookups (counted for SVO_CAST_STATS; dead code elsewhere)
 template <class Mem>
 __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem& mem, const Path& path,
-                                                  const Parent& pfin, const Hit& h, const int32_t l[3], uint32_t ax, int32_t sg) {
+                                                  const Parent& pfin, const Hit& h, const int32_t l[3], uint32_t ax, int32_t sg,
+                                                  uint32_t& loads) {
     const uint32_t face = 2u * ax + (sg < 0 ? 1u : 0u);
     const uint32_t al = ((uint32_t)l[0] & 3u) | (((uint32_t)l[1] & 3u) << 2) | (((uint32_t)l[2] & 3u) << 4);
     const uint2 hd = reinterpret_cast<const uint2*>(P.ao_plan)[face * 64u + al];
@@ -1168,7 +1179,7 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem
         // the brick's corner voxel (wrapped); its solid mask from one lookup
         const uint32_t w[3] = {((hb[0] + (e.x & 255u) - 128u) << 2) & wm, ((hb[1] + ((e.x >> 8) & 255u) - 128u) << 2) & wm,
                                ((hb[2] + ((e.x >> 16) & 255u) - 128u) << 2) & wm};
-        uint64_t m = brick_near(P, mem, path, w, hw, dmax) & vm;
+        uint64_t m = brick_near(P, mem, path, w, hw, dmax, loads) & vm;
         while (m) {  // the plan voxels of this brick that are solid: their samples hit
             const uint32_t v = (uint32_t)__builtin_ctzll(m);
             const uint2 smv = sm[__popcll(vm & ((1ull << v) - 1ull))];
@@ -1201,13 +1212,6 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
     int64_t blk = blockIdx.x;
-    if (P.flags & SVO_CAST_XCD_SWIZZLE) {
-        // blocks are dealt round-robin to the 8 XCDs (blk % 8 share an L2): give each XCD one
-        // contiguous band of tiles so neighbouring tiles hit the same L2
-        const int64_t nb = gridDim.x, per = (nb + 7) / 8, x = blk & 7, k = blk >> 3;
-        const int64_t full = nb - (per - 1) * 8;  // XCDs 0..full-1 receive `per` blocks
-        blk = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
-    }
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
@@ -1225,8 +1229,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         int32_t trl = (int32_t)tq;
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
-        if (P.use_row_order) trl = P.row_order[tq];
-        else if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
+        if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
@@ -1321,7 +1324,9 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
                 const int32_t lx = h.x - (ax == 0u ? st : 0), ly = h.y - (ax == 1u ? st : 0), lz = h.z - (ax == 2u ? st : 0);
                 const int32_t l[3] = {lx, ly, lz};
                 if (P.ao_plan && pfin.sh < 2u * (uint32_t)P.levels && (uint32_t)lx < (1u << 23) && (uint32_t)ly < (1u << 23) && (uint32_t)lz < (1u << 23)) {
-                    cnt = ao_count_plan(P, mem, path, pfin, h, l, ax, -st);
+                    uint32_t aol = 0u;
+                    cnt = ao_count_plan(P, mem, path, pfin, h, l, ax, -st, aol);
+                    if (STATS) atomicAdd(P.stats + 22, (unsigned long long)aol);
                 } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
                 for (int32_t i = 0; i < P.ao_n; i++) {
@@ -1602,19 +1607,6 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
         SVO_FAIL(SVO_ERANGE, "svo_cast_rays: frame too large (2^26 wavefronts or more in one launch)");
     nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
-    if ((d->flags & SVO_CAST_HORIZON_FIRST) && P.tile_rows_local <= kMaxOrderRows) {
-        // shallowest centre ray first (a stable sort of the local rows by |dir.y| of their middle pixel)
-        std::vector<std::pair<float, int32_t>> key(P.tile_rows_local);
-        for (int32_t i = 0; i < P.tile_rows_local; i++) {
-            const int32_t tr = P.tile_row_start + i * P.tile_row_step;
-            float dir[3];
-            raygen_pixel(P.rg, d->width / 2, std::min(tr * 8 + 4, d->height - 1), dir);
-            key[i] = {dir[1] < 0.0f ? -dir[1] : dir[1], i};
-        }
-        std::stable_sort(key.begin(), key.end(), [](const std::pair<float, int32_t>& a, const std::pair<float, int32_t>& b) { return a.first < b.first; });
-        for (int32_t i = 0; i < P.tile_rows_local; i++) P.row_order[i] = (uint16_t)key[i].second;
-        P.use_row_order = 1;
-    }
     return SVO_OK;
 }
 

@@ -100,7 +100,10 @@ SVO_HD float rcp_rn(float x) { return div_rn(1.0f, x); }
 // The same double operations on host and device (no contraction), so both round alike; far cheaper
 // in registers than a libm sin.
 SVO_HD float sin_f32(float xf) {
-    const double x = (double)xf;
+    // (beyond the exact reduction range the argument is first taken modulo fl(2 pi) — an exact remainder
+    // on host and device alike — so the value stays a bounded sine of an equal argument on both)
+    const double x0 = (double)xf;
+    const double x = __builtin_fabs(x0) < 524288.0 ? x0 : __builtin_fmod(x0, 6.283185307179586);
     const double k = __builtin_rint(x * 0.63661977236758134308);
     const double r = (x - k * 1.57079632673412561417e+00) - k * 6.07710050650619224932e-11;
     const double r2 = r * r;
@@ -108,7 +111,12 @@ SVO_HD float sin_f32(float xf) {
                                      r2 * (2.7557319223985893e-06 + r2 * (-2.5052108385441720e-08 + r2 * 1.6059043836821613e-10)))));
     const double cs = 1.0 + r2 * (-0.5 + r2 * (4.1666666666666664e-02 + r2 * (-1.3888888888888889e-03 + r2 * (2.4801587301587302e-05 +
                                   r2 * (-2.7557319223985888e-07 + r2 * (2.0876756987868100e-09 + r2 * -1.1470745597729725e-11))))));
-    const int64_t q = (int64_t)k & 3;
+    // quadrant k mod 4 without an integer conversion of k (undefined for non-finite or huge k): exact
+    // for every finite k (k * 0.25, its floor and 4 * that are exact; k >= 2^54 is a multiple of 4), 0
+    // for NaN / infinite k, whose result is NaN anyway.  The reduction is exact for |k| < 2^20, which
+    // holds on the direct path (|x| < 2^19); host and device take the same operations everywhere.
+    const double kq = k - 4.0 * __builtin_floor(k * 0.25);
+    const int q = (kq >= 0.0 && kq < 4.0) ? (int)kq : 0;
     const double v = (q & 1) ? cs : sn;
     return (float)((q & 2) ? -v : v);
 }

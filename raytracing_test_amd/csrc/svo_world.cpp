@@ -1179,6 +1179,34 @@ extern "C" int svo_tree_load(const char* path, svo_tree** out) {
     }
     for (uint64_t i = 0; i < nm; i++)
         if (t->mats[i] >= npal) SVO_FAIL(SVO_EIO, "svo_tree_load: material out of range");
+    // the structure the kernels assume, walked down from the root with the depth: INTERIOR nodes only
+    // above the brick level, BRICK nodes only at it (levels - 1), SOLID anywhere, and every node reached
+    // at most once (no cycles, no shared subtrees).  Blocks superseded by edits (svo_tree_update) are
+    // unreachable and are not visited.
+    try {
+        std::vector<uint64_t> seen((nn + 63) / 64, 0ull);
+        std::vector<std::pair<uint32_t, int32_t>> stack{{0u, 0}};
+        seen[0] |= 1ull;
+        while (!stack.empty()) {
+            const uint32_t ni = stack.back().first;
+            const int32_t depth = stack.back().second;
+            stack.pop_back();
+            const Node& n = t->nodes[ni];
+            const uint32_t kind = node_kind(n.info);
+            if (kind == K_BRICK && depth != levels - 1) SVO_FAIL(SVO_EIO, "svo_tree_load: brick node above the brick level");
+            if (kind != K_INTERIOR) continue;
+            if (depth >= levels - 1) SVO_FAIL(SVO_EIO, "svo_tree_load: interior node at the brick level");
+            const uint32_t cnt = (uint32_t)__builtin_popcountll(n.mask);
+            for (uint32_t c = 0; c < cnt; c++) {
+                const uint32_t ci = n.ref + c;  // (in range: checked above)
+                if ((seen[ci >> 6] >> (ci & 63u)) & 1ull) SVO_FAIL(SVO_EIO, "svo_tree_load: node reached twice (cycle or shared subtree)");
+                seen[ci >> 6] |= 1ull << (ci & 63u);
+                stack.push_back({ci, depth + 1});
+            }
+        }
+    } catch (const std::bad_alloc&) {
+        SVO_FAIL(SVO_ENOMEM, "svo_tree_load: out of memory");
+    }
     *out = t.release();
     return SVO_OK;
 }

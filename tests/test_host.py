@@ -97,6 +97,11 @@ def test_oracle_sin_is_correctly_rounded(oracle_mod):
     xs = np.concatenate([np.linspace(-300, 300, 60001), np.random.default_rng(3).uniform(-9000, 9000, 20000)]).astype(np.float32)
     got = np.array([oracle_mod.sin_f32(float(x)) for x in xs], np.float32)
     assert np.array_equal(got, np.sin(xs.astype(np.float64)).astype(np.float32))
+    # beyond the exact reduction range (time is caller-given): defined, bounded, NaN only for non-finite x
+    for x in (1e7, -3.3e9, 1e20, -1e30, 3.4e38, -3.4e38):
+        assert -1.0 <= oracle_mod.sin_f32(x) <= 1.0, x
+    for x in (float("inf"), float("-inf"), float("nan")):
+        assert np.isnan(oracle_mod.sin_f32(x))
 
 
 def test_raygen_bit_exact_with_oracle(rt, oracle_mod):
@@ -271,3 +276,37 @@ def test_tree_checkpoint_rejects_damage(rt, ref_tree, tmp_path):
         rt.Tree.load(str(q))
     with pytest.raises(RuntimeError):
         rt.Tree.load(str(tmp_path / "missing.svo"))
+
+    # structural damage under a consistent checksum (every reference in range): node kinds at the
+    # wrong depth, and a child reference back to an ancestor's block (a cycle)
+    def resealed(edit, name):
+        b = bytearray(raw[:-8])
+        edit(b)
+        h = 1469598103934665603
+        for x in b:
+            h = ((h ^ x) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+        q = tmp_path / name
+        q.write_bytes(bytes(b) + struct.pack("<Q", h))
+        return str(q)
+
+    nodes = np.frombuffer(bytes(raw[off:off + 16 * ref_tree.info().n_nodes]), dtype=np.uint32).reshape(-1, 4)
+    kinds = nodes[:, 3] & 3
+    cnt = np.array([bin(int(m)).count("1") for m in (nodes[:, 0].astype(np.uint64) | (nodes[:, 1].astype(np.uint64) << np.uint64(32)))])
+    # a brick whose material run, read as a child block, stays inside the node array (so only the kind check sees it)
+    brick = int(np.nonzero((kinds == 1) & (nodes[:, 2] > 0) & (nodes[:, 2].astype(np.int64) + cnt < len(nodes)))[0][0])
+    inner = int(np.nonzero(kinds[1:] == 0)[0][0]) + 1  # an interior node below the root
+
+    def set_kind(i, k):
+        def f(b):
+            info = struct.unpack_from("<I", b, off + 16 * i + 12)[0]
+            struct.pack_into("<I", b, off + 16 * i + 12, (info & ~3) | k)
+        return f
+
+    def point_back(b):  # an interior node's children = the root's child block
+        struct.pack_into("<I", b, off + 16 * inner + 8, int(nodes[0, 2]))
+
+    for name, edit, msg in (("brick_as_interior.svo", set_kind(brick, 0), "interior node at the brick level"),
+                            ("interior_as_brick.svo", set_kind(inner, 1), "brick node above the brick level"),
+                            ("cycle.svo", point_back, "reached twice")):
+        with pytest.raises(RuntimeError, match=msg):
+            rt.Tree.load(resealed(edit, name))
