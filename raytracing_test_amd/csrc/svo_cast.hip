@@ -87,6 +87,11 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+#ifdef SVO_NO_BRICK_PASS
+constexpr bool kBrickPass = false;  // (A/B: every brick walked voxel by voxel)
+#else
+constexpr bool kBrickPass = true;   // bricks whose path holds no solid voxel are crossed in one move (skip_box PASS)
+#endif
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -376,8 +381,22 @@ __device__ __forceinline__ int32_t seg_cap(double T, float af, float inva) {
 // into cell r + s*i, so the bound seg_cap gave at some earlier state stays s*(rb - r) crossings ahead
 // while the ray has not passed it (every sum up to there is exact, from any state on the way); a
 // negative count means it has, and seg_cap is taken again from the current state
-template <bool TRACK = true, bool RB = false>
-__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) {
+// n - [lane in m] through the borrow-in of one v_subb (the mask in SGPRs)
+__device__ __forceinline__ uint32_t sub_bit(uint32_t x, uint64_t m) {
+    uint32_t r;
+    uint64_t bo;
+    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(bo) : "v"(x), "s"(m));
+    return r;
+}
+
+// PASS (brick pass-through): lanes whose region is a 4^3 brick (bm = its solid mask; empty-box lanes
+// bm = 0) take the move only when no solid voxel lies in the box spanned by the voxels it visits inside
+// the brick — per axis the cells c .. c + s*n' (n' = the axis' crossings, less the exit step on the exit
+// axis), a superset of the path, which is monotone in every coordinate.  The path then holds no solid
+// voxel and the voxel-by-voxel walk would leave the brick at the same state.  (tools/sim_brick_pass.py:
+// about 2/3 of the brick visits of a C3 frame, 92 % of those that do not end in a hit, pass.)
+template <bool TRACK = true, bool RB = false, bool PASS = false>
+__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, uint64_t bm = 0ull, const uint32_t* w = nullptr) {
     // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
 #pragma unroll
@@ -435,6 +454,25 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) 
     // to a negative value, as before commit 1a85dd6) then ends the crossing here — the lanes take their
     // last steps after the traversal loop — instead of growing the budget and never ending the launch.
     if (max((uint32_t)total, max3u((uint32_t)n[0], (uint32_t)n[1], (uint32_t)n[2])) > (uint32_t)R.steps) return false;
+    if (PASS) {
+        // (garbage on bm = 0 lanes: v_bfm / 24-bit multiplies read only the bits they need, no UB)
+        const uint64_t mz = ~(mx | my);
+        const uint32_t np[3] = {sub_bit((uint32_t)n[0], mx), sub_bit((uint32_t)n[1], my), sub_bit((uint32_t)n[2], mz)};
+        uint32_t lo[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const uint32_t c = w[k] & 3u;
+            lo[k] = __builtin_constant_p(R.s[k]) ? (R.s[k] > 0 ? c : c - np[k]) : (R.s[k] > 0 ? c : c - np[k]);
+        }
+        // x range (4 bits) x y rows (nibble bits) -> one 16-bit plane; z planes select the mask's halves
+        const uint32_t rx = bfm(np[0] + 1u, lo[0]), rz = bfm(np[2] + 1u, lo[2]);
+        const uint32_t yr = 0x1111u & bfm((np[1] << 2) + 4u, lo[1] << 2);
+        const uint32_t plane = __umul24(rx, yr);
+        const uint32_t zlo = ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 0u, 1u) & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 1u, 1u) << 16);
+        const uint32_t zhi = ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 2u, 1u) & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 3u, 1u) << 16);
+        const uint32_t f = ((uint32_t)bm & zlo) | ((uint32_t)(bm >> 32) & zhi);
+        if (((f | (f >> 16)) & plane) != 0u) return false;
+    }
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
@@ -459,6 +497,7 @@ struct Stats {
     uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
     uint32_t budget_up;                            // loop iterations that left more budget than they found
+    uint32_t brick_pass;                           // bricks crossed in one move (skip_box PASS)
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -829,7 +868,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -870,32 +909,46 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
         const uint32_t kind = lookup<STATS, !REFLECT, KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
+        const bool brick = kind == R_BRICK;
+        if (STATS && brick) st.bricks++;
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
-        } else if (kind == R_BRICK) {
-            if (STATS) st.bricks++;
+        } else if (brick && !(kBrickPass && fast)) {
             pend = true;
-        } else if (R.steps <= 0) {
+        } else if (!brick && R.steps <= 0) {
             done = true;
-        } else if (!(fast && [&] {
-                       int32_t ex[3];
-                       if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
-                       box_exits(w, R.s, sh, par.mask, ud, ex);
-                       return skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
-                   }())) {
-            if (STATS && fast) st.skip_out++;
-            if (fast) {
-                done = true;  // the budget ends inside this empty box: steps after the loop
-            } else {
-                // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
-                pend = true;
-                bmask = 0ull;
+        } else if (!fast) {
+            // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
+            pend = true;
+            bmask = 0ull;
+        } else {
+            // fast: cross the empty box in one move, or pass the brick when its path holds no solid voxel
+            // (the brick's own box: one 4-voxel cell, exits as box_exits' with t = 1, sh = 2)
+            int32_t ex[3];
+            if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
+            box_exits(w, R.s, sh, par.mask, ud, ex);
+            if (kBrickPass) {
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const int32_t eb = (int32_t)(4u + ~((R.s[k] > 0 ? w[k] : ~w[k]) & 3u));
+                    ex[k] = brick ? eb : ex[k];
+                }
             }
-        } else if (STATS) {
-            st.skips++;
-            st.wv_skips += wave_lead();
-            st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
+            const bool ok = skip_box<TRACK, RB, kBrickPass>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg, brick ? bmask : 0ull, w);
+            if (!ok) {
+                if (brick) {
+                    pend = true;  // a solid voxel may lie on the path (or the budget ends in the brick): walk it
+                } else {
+                    if (STATS) st.skip_out++;
+                    done = true;  // the budget ends inside this empty box: steps after the loop
+                }
+            } else if (STATS) {
+                st.skips++;
+                st.wv_skips += wave_lead();
+                st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
+                st.brick_pass += brick ? 1u : 0u;
+            }
         }
         if (pend) {
             // voxel steps inside the brick, solid mask in registers.  (Postponing bricks until
@@ -1057,6 +1110,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
         if (st.budget_up) atomicAdd(P.stats + 16, (unsigned long long)st.budget_up);
+        atomicAdd(P.stats + 23, (unsigned long long)st.brick_pass);
         if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
     }
     if (!TRACK && R.axis < 3u) {
