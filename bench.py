@@ -228,18 +228,46 @@ def cpu_c1(O, nt):
 
 # ---------------------------------------------------------------------------------- roofline --
 def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
+    """The kernel against the HBM roofline (the contract's "bound": "hbm" — pointer chasing, no MFMA).
+    achieved = algorithmic bytes per ray x rays per launch / average launch time.  Primary rays: SURVEY.md
+    §8(d)'s B_ray (node entries along the reference DDA path, oracle/bray.py).  C4: that, plus the node
+    loads the kernel's AO plan must issue (counted by the SVO_CAST_STATS instance, profiles/bray.json
+    "C4_ao<N>_kernel") and the 1-B AO count — §8(d)'s AO term prices 16 traced AO rays per hit, which the
+    plan replaces by ~6 brick lookups, so it is reported beside the figure, never as it.  A fraction above
+    1 would mean the model prices work the kernel does not do: it is then withheld (null, with the reason)."""
     bray = load_json("bray.json") or {}
-    key = cfg["bray"] if not args.ao else "C4_ao%d" % args.ao
+    key = cfg["bray"]
     b = bray.get(key)
-    if args.shade or b is None:
-        model = None  # §8(d) prices primary traversal (+ AO); the shading pass has no such model
-    else:
+    model, bytes_model, extra = None, None, {}
+    if not args.shade and b is not None:  # (the shading pass has no §8(d) model)
         model = b["bytes_per_ray"]
+        bytes_model = ("SURVEY.md §8d B_ray = 16 (E_child + 1) + 4 E_child + 24 B hit record, E_child = %.2f node entries per ray "
+                       "along the reference DDA path (%s, profiles/bray.json)" % (b["e_child_per_ray"], key))
+        if args.ao:
+            kb = bray.get("C4_ao%d_kernel" % args.ao)
+            traced = bray.get("C4_ao%d" % args.ao)
+            if kb is None:
+                model, bytes_model = None, None
+                extra["note"] = "no committed AO plan load count for %d samples (profiles/bray.json C4_ao%d_kernel)" % (args.ao, args.ao)
+            else:
+                model = b["bytes_per_ray"] + 16.0 * kb["ao_node_loads_per_ray"] + 1.0
+                bytes_model += ("; + 16 B x %.2f AO plan node loads per ray (brick lookups of the per-face plan, counted by the "
+                                "SVO_CAST_STATS instance: profiles/bray.json C4_ao%d_kernel) + 1 B AO count"
+                                % (kb["ao_node_loads_per_ray"], args.ao))
+            if traced is not None:
+                extra["bytes_per_ray_traced_ao_model"] = round(traced["bytes_per_ray"], 2)
+                extra["traced_ao_model"] = ("SURVEY.md §8d with its AO term (16 traced AO rays of 5 steps per hit): not the work "
+                                            "this kernel does, not used for frac")
     achieved = model * rays_per_launch / avg_kernel_s / 1e9 if model else None
-    roof = {"bound": None, "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None, "traffic": None,
-            "bytes_per_ray": round(model, 2) if model else None, "bytes_model": "SURVEY.md §8d (%s, profiles/bray.json)" % key if model else None,
-            "avg_launch_ms": round(avg_kernel_s * 1e3, 4), "rays_per_launch": rays_per_launch}
+    frac = achieved / HBM_PEAK_GBS if achieved else None
+    if frac is not None and frac > 1.0:
+        extra["note"] = ("the bytes model exceeds the HBM peak at this launch time (%.3f): it prices reads the kernel serves "
+                         "from L2 / MALL or does not issue; frac withheld" % frac)
+        frac = None
+    roof = {"bound": "hbm" if model else None, "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(frac, 5) if frac is not None else None, "traffic": None,
+            "bytes_per_ray": round(model, 2) if model else None, "bytes_model": bytes_model,
+            "avg_launch_ms": round(avg_kernel_s * 1e3, 4), "rays_per_launch": rays_per_launch, **extra}
     pmc = load_json("pmc_%s.json" % run_key(args))
     if pmc and pmc.get("rays_per_launch"):
         c = pmc["counters_per_dispatch"]
@@ -254,16 +282,22 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
             "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1),
             "salu_insts_per_wave": round(c["SQ_INSTS_SALU"] / c["SQ_WAVES"], 1) if "SQ_INSTS_SALU" in c else None,
             "valu_issue_frac": round(valu_frac, 4),
-            "bound": "valu-issue" if valu_frac > hbm / HBM_PEAK_GBS else "hbm",
             "counters": "profiles/pmc_%s.json (rocprofv3 --pmc passes, tools/pmc.sh%s)" % (run_key(args), "; scaled per ray to this launch"
                                                                                           if world > 1 or scale != 1 else ""),
             "valu_issue_rule": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz x launch time)" % (VALU_CYCLES, N_SIMD, CLOCK_GHZ),
         })
-    elif model:
-        roof["bound"] = "hbm"  # the §8(d) model's bound; no counters committed for this config
-    if roof["frac"] is not None and roof["frac"] > 1.0:
-        roof["note"] = ("the §8(d) algorithmic bytes exceed the HBM peak: the nodes they count are served from L2 / MALL "
-                        "(the measured HBM traffic is hbm_gbs_measured)")
+        sq = load_json("sq_%s.json" % run_key(args))
+        if sq:
+            q = sq["counters_per_dispatch"]
+            wc = q["SQ_WAVE_CYCLES"]
+            roof["limiter"] = ("dependent instruction chains: of the wave-cycles %.0f %% issue, %.0f %% wait to issue, %.0f %% wait on "
+                               "memory (SQ counters, profiles/sq_%s.json); VALU issue %.2f of peak; measured HBM traffic %.1f %% of peak "
+                               "(the nodes the bytes model counts are served from L2 / MALL)"
+                               % (100.0 * q["SQ_ACTIVE_INST_ANY"] / wc, 100.0 * q["SQ_WAIT_INST_ANY"] / wc, 100.0 * q["SQ_WAIT_ANY"] / wc,
+                                  run_key(args), valu_frac, 100.0 * hbm / HBM_PEAK_GBS))
+        else:
+            roof["limiter"] = ("instruction stream: VALU issue %.2f of peak, measured HBM traffic %.1f %% of peak (the nodes the model "
+                               "counts are served from L2 / MALL)" % (valu_frac, 100.0 * hbm / HBM_PEAK_GBS))
     return roof
 
 
@@ -738,6 +772,8 @@ def print_stats(rt, tree, d0, out, stream, torch):
         if os.environ.get("SVO_STAMPS"):  # per-block start / end stamps (dispatch order) for offline analysis
             np.save(os.environ["SVO_STAMPS"], stamps)
         stamps = stamps[stamps[:, 1] > 0].astype(np.float64) / 100.0  # launched blocks; us (100 MHz)
+        if len(stamps) == 0:  # (the AO instances keep no timeline)
+            continue
         t0s = stamps[:, 0].min()
         dur = stamps[:, 1] - stamps[:, 0]
         span = stamps[:, 1].max() - t0s

@@ -87,6 +87,9 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+#ifndef SVO_BRICK_PASS_TEST
+#define SVO_BRICK_PASS_TEST 0  // 0: the box of the path's cells; 1: its y rows only (A/B)
+#endif
 #ifdef SVO_NO_BRICK_PASS
 constexpr bool kBrickPass = false;  // (A/B: every brick walked voxel by voxel)
 #else
@@ -396,7 +399,7 @@ __device__ __forceinline__ uint32_t sub_bit(uint32_t x, uint64_t m) {
 // voxel and the voxel-by-voxel walk would leave the brick at the same state.  (tools/sim_brick_pass.py:
 // about 2/3 of the brick visits of a C3 frame, 92 % of those that do not end in a hit, pass.)
 template <bool TRACK = true, bool RB = false, bool PASS = false>
-__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, uint64_t bm = 0ull, const uint32_t* w = nullptr) {
+__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, uint64_t bm = 0ull, const uint32_t* w = nullptr, bool pass_wave = false) {
     // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
 #pragma unroll
@@ -454,15 +457,23 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, 
     // to a negative value, as before commit 1a85dd6) then ends the crossing here — the lanes take their
     // last steps after the traversal loop — instead of growing the budget and never ending the launch.
     if (max((uint32_t)total, max3u((uint32_t)n[0], (uint32_t)n[1], (uint32_t)n[2])) > (uint32_t)R.steps) return false;
-    if (PASS) {
+    if (PASS && pass_wave) {  // (wave-uniform: the wave holds a lane passing a brick)
         // (garbage on bm = 0 lanes: v_bfm / 24-bit multiplies read only the bits they need, no UB)
+#if SVO_BRICK_PASS_TEST == 1
+        // y rows only: the voxels of the brick's rows the path visits (every x, z) — a looser box, 8 VALU
+        const uint32_t ny = sub_bit((uint32_t)n[1], my);
+        const uint32_t cy = w[1] & 3u;
+        const uint32_t loy = R.s[1] > 0 ? cy : cy - ny;
+        const uint32_t r16 = bfm((ny << 2) + 4u, loy << 2);
+        if ((((uint32_t)bm | (uint32_t)(bm >> 32)) & (r16 | (r16 << 16))) != 0u) return false;
+#else
         const uint64_t mz = ~(mx | my);
         const uint32_t np[3] = {sub_bit((uint32_t)n[0], mx), sub_bit((uint32_t)n[1], my), sub_bit((uint32_t)n[2], mz)};
         uint32_t lo[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const uint32_t c = w[k] & 3u;
-            lo[k] = __builtin_constant_p(R.s[k]) ? (R.s[k] > 0 ? c : c - np[k]) : (R.s[k] > 0 ? c : c - np[k]);
+            lo[k] = R.s[k] > 0 ? c : c - np[k];
         }
         // x range (4 bits) x y rows (nibble bits) -> one 16-bit plane; z planes select the mask's halves
         const uint32_t rx = bfm(np[0] + 1u, lo[0]), rz = bfm(np[2] + 1u, lo[2]);
@@ -472,6 +483,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, 
         const uint32_t zhi = ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 2u, 1u) & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 3u, 1u) << 16);
         const uint32_t f = ((uint32_t)bm & zlo) | ((uint32_t)(bm >> 32) & zhi);
         if (((f | (f >> 16)) & plane) != 0u) return false;
+#endif
     }
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -928,14 +940,16 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             int32_t ex[3];
             if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
             box_exits(w, R.s, sh, par.mask, ud, ex);
-            if (kBrickPass) {
+            const bool pass_wave = kBrickPass && __ballot(brick) != 0ull;  // (wave-uniform)
+            if (pass_wave) {
 #pragma unroll
                 for (int k = 0; k < 3; k++) {
                     const int32_t eb = (int32_t)(4u + ~((R.s[k] > 0 ? w[k] : ~w[k]) & 3u));
                     ex[k] = brick ? eb : ex[k];
                 }
             }
-            const bool ok = skip_box<TRACK, RB, kBrickPass>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg, brick ? bmask : 0ull, w);
+            const bool ok = skip_box<TRACK, RB, kBrickPass>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg, brick ? bmask : 0ull, w,
+                                                            pass_wave);
             if (!ok) {
                 if (brick) {
                     pend = true;  // a solid voxel may lie on the path (or the budget ends in the brick): walk it

@@ -55,10 +55,15 @@ def test_roofline_model_and_counters(bench):
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-4
     pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_c3.json")))
     assert r["traffic"] == round(pmc["hbm_bytes_per_launch"])  # the same rays per launch: unscaled
-    assert r["bound"] == ("valu-issue" if r["valu_issue_frac"] > r["hbm_frac_measured"] else "hbm")
-    # C4 prices the AO rays' node entries too; a shaded line has no §8(d) model
+    assert r["bound"] == "hbm" and "wait to issue" in r["limiter"]  # (the contract's roofline; the SQ counters name the limiter)
+    # C4: the primary bytes + the AO plan's node loads (not the traced-AO model, which is reported beside it)
     r4 = bench.roofline(_args(ao=16), cfg, 2073600, 0.31e-3, 1)
-    assert abs(r4["bytes_per_ray"] - bray["C4_ao16"]["bytes_per_ray"]) < 0.01 and r4["bytes_per_ray"] > r["bytes_per_ray"]
+    kb = bray["C4_ao16_kernel"]["ao_node_loads_per_ray"]
+    assert abs(r4["bytes_per_ray"] - (b + 16 * kb + 1)) < 0.01 and r4["bytes_per_ray"] > r["bytes_per_ray"]
+    assert abs(r4["bytes_per_ray_traced_ao_model"] - bray["C4_ao16"]["bytes_per_ray"]) < 0.01
+    # a fraction above 1 is never published
+    rf = bench.roofline(_args(), cfg, 2073600, 0.05e-3, 1)
+    assert rf["frac"] is None and "withheld" in rf["note"]
     rs = bench.roofline(_args(shade=True), cfg, 2073600, 1.3e-3, 1)
     assert rs["frac"] is None and rs["bytes_per_ray"] is None
     # counters measured at N = 1 scale per ray to another launch size (a rank's shard)
