@@ -450,6 +450,12 @@ def main():
             xmode, xnote = "torch", "svo_exchange_create failed (%s); torch.distributed all_to_all used" % e
         if exch is not None and n_own:
             frames_out = rt.Tree.alloc_hits(n_own * W * H, dev, ao=args.ao > 0)
+    # the C-ABI exchange casts straight into wire records (svo_cast_wire: 8 B per ray from integral camera
+    # positions, else 12 B) and decodes them on the display rank (svo_exchange_wire): no hit records, no pack
+    wires = None
+    if exch is not None:
+        wb = tree.wire_bytes(desc)
+        wires = [torch.empty((rays_per_launch, wb), dtype=torch.uint8, device=gdev) for _ in range(nbuf)]
 
     # torch exchange (shading image, gloo rehearsal, or --exchange torch): frame f -> rank f % world
     counts = [shard.shard_count(W, H, r, world) for r in range(world)]
@@ -473,6 +479,8 @@ def main():
             if args.shade:
                 # the image is the product: no hit records, so rays that provably leave the scene upwards stop early
                 tree.shade(desc, outs[b]["rgba"], out=None, stream=stream, scene=scene)
+            elif wires is not None:
+                tree.cast_wire(desc, wires[b], outs[b].get("ao"), stream)
             else:
                 tree.cast(desc, outs[b], stream)
             if ev is not None:
@@ -482,7 +490,7 @@ def main():
         if xmode == "capi":
             cast_done[b].record(stream)
             xstream.wait_event(cast_done[b])
-            exch.frames(tree, desc, outs[b], frames_out, xstream)
+            exch.wire(tree, desc, wires[b], frames_out, ao=outs[b].get("ao"), stream=xstream)
             e = torch.cuda.Event()
             e.record(xstream)
             xdone[b] = e
@@ -617,11 +625,13 @@ def main():
                    "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "gather": gather,
                    "dispatch_order": "top tile rows first",
                    "exchange": None if not gather else (
-                       ("svo_exchange_frames (C ABI, RCCL send/recv group): 12-B wire records" + (" + AO counts" if args.ao else "") +
-                        ", frame f to rank f %% N, unpacked on arrival, on a second stream overlapping the next cast")
+                       ("svo_cast_wire + svo_exchange_wire (C ABI, RCCL send/recv group): %d-B wire records written by the cast "
+                        "kernel" % tree.wire_bytes(desc) + (" + AO counts" if args.ao else "") +
+                        ", frame f to rank f % N (own shards decoded in place), decoded on arrival on a second stream "
+                        "overlapping the next cast")
                        if xmode == "capi" else
                        ("torch.distributed all_to_all_single: " + ("rgba image" if args.shade else "12-B wire hit records") +
-                        ", frame f to rank f %% N" + ("; " + xnote if xnote else ""))),
+                        ", frame f to rank f % N" + ("; " + xnote if xnote else ""))),
                    "tree_nodes": info.n_nodes, "tree_bytes": info.n_nodes * 16 + info.n_mat_bytes, "tree_build_s": round(build_s, 3),
                    "tree_builder": builder, **({"scene_nodes": scene.info().n_nodes} if scene is not None else {})},
         "roofline": roof,

@@ -23,10 +23,11 @@
 extern "C" {
 #endif
 
-#define SVO_RT_VERSION 6  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
+#define SVO_RT_VERSION 7  /* 2: svo_cast_desc.n_frames / frame_origins, wire records; 3: svo_exchange_*, 64-bit node addressing;
                              4: tree views (liquid stored for the shading pass), svo_shade_desc.scene / time;
                              6: svo_tree_save / svo_tree_load (5, a cost-ordered dispatch, was measured slower
-                             and removed) */
+                             and removed); 7: 8-B compact wire records, svo_wire_bytes / svo_cast_wire /
+                             svo_wire_scatter / svo_exchange_wire */
 
 enum {
     SVO_OK = 0,
@@ -203,8 +204,9 @@ typedef struct {
                           skips that ran out of budget, brick voxel steps, plain voxel steps,
                           lane work units, wave-max work units x 64, crossings by box cell
                           size (4 slots), brick visits, wave-level loop iterations,
-                          wave-level brick voxel steps, loop iterations that left a ray
-                          more budget than they found (0 by construction), lookups started at
+                          wave-level brick voxel steps, loop iterations that took no DDA
+                          step and were ended by the progress guard (0 unless a count is wrong),
+                          lookups started at
                           the root, lookups answered by the cached parent, wave-level
                           crossings, wave-level descent levels, lookups restarted from the
                           per-lane path, node loads of the AO plan's brick lookups;
@@ -265,17 +267,32 @@ int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir
                           svo_block* block);
 int svo_sync(void* hip_stream);
 
-/* Wire format of hit records for the exchange between GPUs (the tile-row gather), 12 B per ray:
-     int16 dx, dy, dz   pos - trunc(origin of the ray's frame, or of the explicit ray)
-     uint16 info16      hit << 15 | axis << 13 | (step < 0) << 12 | material id (12 bits)
-     float t
+/* Wire formats of hit records for the exchange between GPUs (the tile-row gather):
+   12 B (any desc)  int16 dx, dy, dz   pos - trunc(origin of the ray's frame, or of the explicit ray)
+                    uint16 info16      hit << 15 | axis << 13 | (step < 0) << 12 | material id (12 bits)
+                    float t
+   8 B (compact)    u64: n_x | n_y << 15 | n_z << 30 | hit << 45 | axis << 46 | material id << 48, n_k = the DDA
+                    steps the ray took on axis k.  Used for frame descs whose every camera position is integral
+                    or half-integral: the receiver regenerates each pixel's ray and recovers the step signs,
+                    the position, the steps left and t exactly (every crossing sum from such origins is exact).
    stepsLeft is not sent: every DDA step moves one axis by one voxel, so a hit leaves
-   steps - |dx| - |dy| - |dz| and a miss 0.  Needs steps <= 32767 and fewer than 4096 palette
-   entries (SVO_ERANGE otherwise).  d describes the records (svo_cast_count of them, the
-   frames / origins they were cast from); wire and hits are device buffers; asynchronous. */
-#define SVO_WIRE_BYTES 12
+   steps - |dx| - |dy| - |dz| and a miss 0.  Both need steps <= 32767 and at most 4096 palette entries
+   (SVO_ERANGE otherwise).  svo_wire_bytes gives a desc's record size (8 or 12).  d describes the
+   records (svo_cast_count of them, the frames / origins and tile rows they were cast from); wire and
+   hits are device buffers; asynchronous. */
+#define SVO_WIRE_BYTES 12 /* the larger of the two */
+int svo_wire_bytes(const svo_tree* t, const svo_cast_desc* d, int32_t* bytes);
 int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const svo_hits* hits, void* wire, void* hip_stream);
 int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* hip_stream);
+/* svo_cast_rays writing the wire record of each ray (svo_wire_bytes(d) bytes, record order) instead of its hit
+   record — the cast and the pack in one pass; ao: the AO counts as svo_hits.ao (when d->ao_samples > 0) */
+int svo_cast_wire(const svo_tree* t, const svo_cast_desc* d, void* wire, uint8_t* ao, void* hip_stream);
+/* decode the wire records of the shard d describes (tile rows tile_row_start, +tile_row_step, ... of its
+   n_frames frames) into whole frames: frames holds n_frames x width x height records in pixel order (the
+   layout of an unsharded svo_cast_rays); only this shard's pixels are written.  ao: AO counts in record
+   order (or NULL) */
+int svo_wire_scatter(const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao, const svo_hits* frames,
+                     void* hip_stream);
 
 /* ------------------------------------------------------------- multi-GPU frame exchange ----- */
 /* frames sharded by interleaved 8-pixel tile rows (svo_cast_desc.tile_row_start = rank,
@@ -292,15 +309,21 @@ int svo_exchange_wrap(void* nccl_comm, int32_t device, svo_exchange** out);
 void svo_exchange_destroy(svo_exchange* x);
 int svo_exchange_info(const svo_exchange* x, int32_t* rank, int32_t* nranks);
 /* One step's exchange.  d: this rank's shard of n_frames frames (as cast into `mine`, records of frame f
-   after those of frame f-1); frame f is displayed by rank f % nranks.  Packs `mine` into 12-B wire
-   records (svo_hits_pack; AO counts alongside when d->ao_samples > 0), sends every frame's shard to its
+   after those of frame f-1); frame f is displayed by rank f % nranks.  Packs `mine` into wire records
+   (svo_hits_pack; AO counts alongside when d->ao_samples > 0), sends every frame's shard to its
    display rank and receives the shards of the frames this rank displays — one RCCL group of
    point-to-point transfers: a gather for one frame, an all-to-all for nranks frames — then unpacks them
    into frames_out: the whole frames (width x height records each, the layout of an unsharded
    svo_cast_rays) of frames rank, rank + nranks, ... in that order (unused on ranks that display none).
+   This rank's own shards of its frames never travel.  Returns SVO_EINVAL when t lives on another device.
    Asynchronous on hip_stream; `mine` must not be overwritten before the stream passes this call. */
 int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const svo_hits* mine, const svo_hits* frames_out,
                         void* hip_stream);
+/* the same exchange from wire records this rank cast itself (svo_cast_wire of d into `wire`, with `ao` when
+   d->ao_samples > 0): no pack pass; the records of the frames this rank displays are decoded from `wire`
+   in place (they never travel).  `wire` and `ao` must not be overwritten before the stream passes this call. */
+int svo_exchange_wire(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao,
+                      const svo_hits* frames_out, void* hip_stream);
 
 /* ---------------------------------------------------------------------------- shading ------- */
 /* Shading pass: low_res.frag's colour model over castRayFromCam hits, one float4

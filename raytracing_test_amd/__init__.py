@@ -44,11 +44,11 @@ CAST_NO_OCTANT = 16384  # per-wave step-sign flags instead of the launch's compi
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
-              "budget_grew", "root_starts", "cache_empty", "wave_skips", "wave_descents",
+              "no_progress", "root_starts", "cache_empty", "wave_skips", "wave_descents",
               "path_starts", "ao_node_loads")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
-WIRE_BYTES = 12  # SVO_WIRE_BYTES: one hit record in the exchange format (svo_hits_pack)
+WIRE_BYTES = 12  # SVO_WIRE_BYTES: the larger wire record (12 B general, 8 B compact: Tree.wire_bytes(desc))
 VIEW_SOLID, VIEW_ALL = 0, 1  # SVO_VIEW_*: castRayFromCam's blocks / every stored block (the shading scene)
 
 
@@ -138,7 +138,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
-    "svo_tree_save", "svo_tree_load",
+    "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire",
 )
 
 
@@ -174,7 +174,10 @@ def lib():
     # library builds of earlier revisions (tools/build_variant.py) loads them through this module)
     for name, at in (("svo_build_view", [vp, i32, C.POINTER(vp)]), ("svo_build_terrain_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
                      ("svo_build_terrain_gpu_view", [i32, i32, i32, i32, i32, C.POINTER(vp)]),
-                     ("svo_tree_save", [vp, C.c_char_p]), ("svo_tree_load", [C.c_char_p, C.POINTER(vp)])):
+                     ("svo_tree_save", [vp, C.c_char_p]), ("svo_tree_load", [C.c_char_p, C.POINTER(vp)]),
+                     ("svo_wire_bytes", [vp, C.POINTER(CastDesc), C.POINTER(i32)]), ("svo_cast_wire", [vp, C.POINTER(CastDesc), vp, vp, vp]),
+                     ("svo_wire_scatter", [vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
+                     ("svo_exchange_wire", [vp, vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -548,15 +551,36 @@ class Tree:
             out["ao"] = torch.empty(n, dtype=torch.uint8, device=dev)
         return out
 
+    def wire_bytes(self, desc):
+        """bytes per wire record of desc's records: 8 (compact: frames from integral / half-integral camera
+        positions) or 12 (include/svo_rt.h)"""
+        b = C.c_int32()
+        _check(lib().svo_wire_bytes(self._h, C.byref(desc), C.byref(b)), "svo_wire_bytes")
+        return b.value
+
+    def cast_wire(self, desc, wire, ao=None, stream=None):
+        """svo_cast_wire: cast desc's rays straight into wire records (uint8 device tensor of count x
+        wire_bytes), AO counts into `ao` (uint8 device tensor) when desc.ao_samples > 0"""
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_cast_wire(self._h, C.byref(desc), C.c_void_p(wire.data_ptr()), C.c_void_p(ao.data_ptr()) if ao is not None else None,
+                                   C.c_void_p(s) if s else None), "svo_cast_wire")
+
+    def wire_scatter(self, desc, wire, frames, ao=None, stream=None):
+        """svo_wire_scatter: the shard desc's wire records into whole frames (desc.n_frames x W x H records,
+        pixel order); only the shard's pixels are written"""
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_wire_scatter(self._h, C.byref(desc), C.c_void_p(wire.data_ptr()), C.c_void_p(ao.data_ptr()) if ao is not None else None,
+                                      C.byref(_hits(frames)), C.c_void_p(s) if s else None), "svo_wire_scatter")
+
     def pack_hits(self, desc, out, wire, stream=None):
-        """hit records (device) -> the 12-B wire records of include/svo_rt.h in `wire` (uint8 tensor)"""
+        """hit records (device) -> the wire records of include/svo_rt.h in `wire` (uint8 tensor, wire_bytes(desc) per record)"""
         h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), None)
         s = getattr(stream, "cuda_stream", stream)
         _check(lib().svo_hits_pack(self._h, C.byref(desc), C.byref(h), C.c_void_p(wire.data_ptr()), C.c_void_p(s) if s else None),
                "svo_hits_pack")
 
     def unpack_hits(self, desc, wire, out, stream=None):
-        """12-B wire records -> hit records (device)"""
+        """wire records -> hit records (device), record order"""
         h = Hits(out["pos_steps"].data_ptr(), out["t"].data_ptr(), out["info"].data_ptr(), None)
         s = getattr(stream, "cuda_stream", stream)
         _check(lib().svo_hits_unpack(self._h, C.byref(desc), C.c_void_p(wire.data_ptr()), C.byref(h), C.c_void_p(s) if s else None),
@@ -693,6 +717,15 @@ class Exchange:
         fo = _hits(frames_out)
         _check(lib().svo_exchange_frames(self._h, tree._h, C.byref(desc), C.byref(_hits(mine)), C.byref(fo) if fo else None,
                                          C.c_void_p(s) if s else None), "svo_exchange_frames")
+
+    def wire(self, tree, desc, wire, frames_out, ao=None, stream=None):
+        """One step's exchange from wire records this rank cast itself (Tree.cast_wire of desc into `wire`):
+        svo_exchange_wire, asynchronous on `stream`."""
+        s = getattr(stream, "cuda_stream", stream)
+        fo = _hits(frames_out)
+        _check(lib().svo_exchange_wire(self._h, tree._h, C.byref(desc), C.c_void_p(wire.data_ptr()),
+                                       C.c_void_p(ao.data_ptr()) if ao is not None else None, C.byref(fo) if fo else None,
+                                       C.c_void_p(s) if s else None), "svo_exchange_wire")
 
 
 def sun_dir():

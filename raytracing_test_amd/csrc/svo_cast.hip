@@ -21,6 +21,7 @@
 #include "../../include/svo_rt.h"
 #include "svo_hip.h"
 #include "svo_internal.h"
+#include "svo_wire.h"
 
 using namespace svo;
 
@@ -67,6 +68,8 @@ struct CastParams {
     float* t;
     uint32_t* info;
     uint8_t* ao;
+    uint32_t* wire;        // svo_cast_wire: the wire record of each ray instead of its hit record (svo_wire.h)
+    int32_t wire_compact;  // 8-B records
     // hemisphere AO (A8)
     int32_t ao_n, ao_steps;
     float ao_tab[3 * 64];
@@ -87,14 +90,6 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
-#ifndef SVO_BRICK_PASS_TEST
-#define SVO_BRICK_PASS_TEST 0  // 0: the box of the path's cells; 1: its y rows only (A/B)
-#endif
-#ifdef SVO_NO_BRICK_PASS
-constexpr bool kBrickPass = false;  // (A/B: every brick walked voxel by voxel)
-#else
-constexpr bool kBrickPass = true;   // bricks whose path holds no solid voxel are crossed in one move (skip_box PASS)
-#endif
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -336,9 +331,6 @@ __device__ __forceinline__ int32_t count_est(double T, double a, float inva, dou
     return (int32_t)mu;
 }
 
-// (v_max3_u32)
-__device__ __forceinline__ uint32_t max3u(uint32_t a, uint32_t b, uint32_t c) { return max(a, max(b, c)); }
-
 // Exact segments.  From any state (T, a), the crossings T + i*a are multiples of 2^v, v = the lower
 // of the lowest set bits of T and a, so every crossing below B = 2^(v+53) is exact and representable,
 // and the first one at or above B is that sum rounded once, as fma(i, a, T) computes it too.  B is at
@@ -384,22 +376,8 @@ __device__ __forceinline__ int32_t seg_cap(double T, float af, float inva) {
 // into cell r + s*i, so the bound seg_cap gave at some earlier state stays s*(rb - r) crossings ahead
 // while the ray has not passed it (every sum up to there is exact, from any state on the way); a
 // negative count means it has, and seg_cap is taken again from the current state
-// n - [lane in m] through the borrow-in of one v_subb (the mask in SGPRs)
-__device__ __forceinline__ uint32_t sub_bit(uint32_t x, uint64_t m) {
-    uint32_t r;
-    uint64_t bo;
-    asm("v_subb_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(bo) : "v"(x), "s"(m));
-    return r;
-}
-
-// PASS (brick pass-through): lanes whose region is a 4^3 brick (bm = its solid mask; empty-box lanes
-// bm = 0) take the move only when no solid voxel lies in the box spanned by the voxels it visits inside
-// the brick — per axis the cells c .. c + s*n' (n' = the axis' crossings, less the exit step on the exit
-// axis), a superset of the path, which is monotone in every coordinate.  The path then holds no solid
-// voxel and the voxel-by-voxel walk would leave the brick at the same state.  (tools/sim_brick_pass.py:
-// about 2/3 of the brick visits of a C3 frame, 92 % of those that do not end in a hit, pass.)
-template <bool TRACK = true, bool RB = false, bool PASS = false>
-__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, uint64_t bm = 0ull, const uint32_t* w = nullptr, bool pass_wave = false) {
+template <bool TRACK = true, bool RB = false>
+__device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg) {
     // exits beyond the budget are clamped (safe: total > steps)
     int32_t e[3];
 #pragma unroll
@@ -451,40 +429,7 @@ __device__ __forceinline__ bool skip_box(Ray& R, const int32_t ex[3], bool seg, 
     n[1] = add_bit(n[1], __ballot(F[1] < next_if(V, mx)) | my);
     n[2] = add_bit(n[2], __ballot(F[2] <= V));
     const int32_t total = n[0] + n[1] + n[2];
-    // Budget guard by construction: every count is at most its axis' clamped exit e[k] + 1 <= steps + 1
-    // (and the steps are below 2^20 on this path), so the move is taken only when each count, and the
-    // total, fits the steps left as unsigned values.  A count estimate gone wrong (saturated, or wrapped
-    // to a negative value, as before commit 1a85dd6) then ends the crossing here — the lanes take their
-    // last steps after the traversal loop — instead of growing the budget and never ending the launch.
-    if (max((uint32_t)total, max3u((uint32_t)n[0], (uint32_t)n[1], (uint32_t)n[2])) > (uint32_t)R.steps) return false;
-    if (PASS && pass_wave) {  // (wave-uniform: the wave holds a lane passing a brick)
-        // (garbage on bm = 0 lanes: v_bfm / 24-bit multiplies read only the bits they need, no UB)
-#if SVO_BRICK_PASS_TEST == 1
-        // y rows only: the voxels of the brick's rows the path visits (every x, z) — a looser box, 8 VALU
-        const uint32_t ny = sub_bit((uint32_t)n[1], my);
-        const uint32_t cy = w[1] & 3u;
-        const uint32_t loy = R.s[1] > 0 ? cy : cy - ny;
-        const uint32_t r16 = bfm((ny << 2) + 4u, loy << 2);
-        if ((((uint32_t)bm | (uint32_t)(bm >> 32)) & (r16 | (r16 << 16))) != 0u) return false;
-#else
-        const uint64_t mz = ~(mx | my);
-        const uint32_t np[3] = {sub_bit((uint32_t)n[0], mx), sub_bit((uint32_t)n[1], my), sub_bit((uint32_t)n[2], mz)};
-        uint32_t lo[3];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const uint32_t c = w[k] & 3u;
-            lo[k] = R.s[k] > 0 ? c : c - np[k];
-        }
-        // x range (4 bits) x y rows (nibble bits) -> one 16-bit plane; z planes select the mask's halves
-        const uint32_t rx = bfm(np[0] + 1u, lo[0]), rz = bfm(np[2] + 1u, lo[2]);
-        const uint32_t yr = 0x1111u & bfm((np[1] << 2) + 4u, lo[1] << 2);
-        const uint32_t plane = __umul24(rx, yr);
-        const uint32_t zlo = ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 0u, 1u) & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 1u, 1u) << 16);
-        const uint32_t zhi = ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 2u, 1u) & 0xFFFFu) | ((uint32_t)__builtin_amdgcn_sbfe((int32_t)rz, 3u, 1u) << 16);
-        const uint32_t f = ((uint32_t)bm & zlo) | ((uint32_t)(bm >> 32) & zhi);
-        if (((f | (f >> 16)) & plane) != 0u) return false;
-#endif
-    }
+    if (total > R.steps) return false;  // (a wrong count cannot hang the launch either: trace's progress guard)
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         R.T[k] = on_grid(R.T[k], n[k], R.a(k));
@@ -508,8 +453,7 @@ struct Stats {
                                         // parent mask
     uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
-    uint32_t budget_up;                            // loop iterations that left more budget than they found
-    uint32_t brick_pass;                           // bricks crossed in one move (skip_box PASS)
+    uint32_t no_progress;                          // loop iterations that consumed no budget (the guard's trips: 0)
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -880,7 +824,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -907,7 +851,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     while (!done) {
         // the voxel just entered is untested
         if (STATS) st.wv_iters += wave_lead();
-        const int32_t steps_in = R.steps;  // (STATS: the budget never grows)
+        const int32_t steps_in = R.steps;  // (the progress guard below)
         uint32_t w[3];
         wrap3(R, wm, w);
         if (ESCAPE && top >= 0 && R.s[1] > 0 && (int32_t)w[1] > top && (int64_t)w[1] + R.steps <= (int64_t)wm) {
@@ -921,48 +865,32 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
         const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
         const uint32_t kind = lookup<STATS, !REFLECT, KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
-        const bool brick = kind == R_BRICK;
-        if (STATS && brick) st.bricks++;
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
-        } else if (brick && !(kBrickPass && fast)) {
+        } else if (kind == R_BRICK) {
+            if (STATS) st.bricks++;
             pend = true;
-        } else if (!brick && R.steps <= 0) {
+        } else if (R.steps <= 0) {
             done = true;
-        } else if (!fast) {
-            // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
-            pend = true;
-            bmask = 0ull;
-        } else {
-            // fast: cross the empty box in one move, or pass the brick when its path holds no solid voxel
-            // (the brick's own box: one 4-voxel cell, exits as box_exits' with t = 1, sh = 2)
-            int32_t ex[3];
-            if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
-            box_exits(w, R.s, sh, par.mask, ud, ex);
-            const bool pass_wave = kBrickPass && __ballot(brick) != 0ull;  // (wave-uniform)
-            if (pass_wave) {
-#pragma unroll
-                for (int k = 0; k < 3; k++) {
-                    const int32_t eb = (int32_t)(4u + ~((R.s[k] > 0 ? w[k] : ~w[k]) & 3u));
-                    ex[k] = brick ? eb : ex[k];
-                }
+        } else if (!(fast && [&] {
+                       int32_t ex[3];
+                       if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
+                       box_exits(w, R.s, sh, par.mask, ud, ex);
+                       return skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
+                   }())) {
+            if (STATS && fast) st.skip_out++;
+            if (fast) {
+                done = true;  // the budget ends inside this empty box: steps after the loop
+            } else {
+                // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
+                pend = true;
+                bmask = 0ull;
             }
-            const bool ok = skip_box<TRACK, RB, kBrickPass>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg, brick ? bmask : 0ull, w,
-                                                            pass_wave);
-            if (!ok) {
-                if (brick) {
-                    pend = true;  // a solid voxel may lie on the path (or the budget ends in the brick): walk it
-                } else {
-                    if (STATS) st.skip_out++;
-                    done = true;  // the budget ends inside this empty box: steps after the loop
-                }
-            } else if (STATS) {
-                st.skips++;
-                st.wv_skips += wave_lead();
-                st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
-                st.brick_pass += brick ? 1u : 0u;
-            }
+        } else if (STATS) {
+            st.skips++;
+            st.wv_skips += wave_lead();
+            st.skip_by_sh[min(3u, (sh >> 1) - 1u)]++;
         }
         if (pend) {
             // voxel steps inside the brick, solid mask in registers.  (Postponing bricks until
@@ -1086,7 +1014,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 }
             }
         }
-        if (STATS && R.steps > steps_in) st.budget_up++;
+        // Progress guard, by construction: every iteration that does not end the ray takes at least one
+        // DDA step (a crossing takes its exit step, a brick walk its first step, a reflection / refraction
+        // its next one), so the budget strictly decreases.  An iteration that left the budget where it was,
+        // or grew it — only a wrong crossing count could (a saturated or wrapped estimate, as before commit
+        // 1a85dd6) — ends the ray: the launch always ends.  (STATS counts the trips: 0 in every test.)
+        if (R.steps >= steps_in && !done) {
+            if (STATS) st.no_progress++;
+            done = true;
+        }
     }
     const bool hit = mat != kNoHit;
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
@@ -1123,8 +1059,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 19, (unsigned long long)st.wv_skips);
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
-        if (st.budget_up) atomicAdd(P.stats + 16, (unsigned long long)st.budget_up);
-        atomicAdd(P.stats + 23, (unsigned long long)st.brick_pass);
+        if (st.no_progress) atomicAdd(P.stats + 16, (unsigned long long)st.no_progress);
         if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
     }
     if (!TRACK && R.axis < 3u) {
@@ -1380,9 +1315,13 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         Parent pfin;
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
-        reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
-        P.t[out] = h.t;
-        P.info[out] = h.info;
+        if (!SHADE && P.wire) {  // (wave-uniform: one launch writes one kind of record)
+            wire_put(P.wire, P.wire_compact != 0, out, o, h.x, h.y, h.z, h.t, h.info);
+        } else {
+            reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
+            P.t[out] = h.t;
+            P.info[out] = h.info;
+        }
         if (AO) {
             // AO rays from the centre of lastPos, pole turned to the hit face's normal (A8)
             uint32_t cnt = 0u;
@@ -1866,9 +1805,25 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     return SVO_OK;
 }
 
+static int cast_launch(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, void* wire, void* stream);
+
 extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, void* stream) {
     if (!t || !d || !o) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL argument");
     if (!o->pos_steps || !o->t || !o->info) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: NULL output buffer");
+    return cast_launch(t, d, o, nullptr, stream);
+}
+
+extern "C" int svo_cast_wire(const svo_tree* t, const svo_cast_desc* d, void* wire, uint8_t* ao, void* stream) {
+    if (!t || !d || !wire) SVO_FAIL(SVO_EINVAL, "svo_cast_wire: NULL argument");
+    if (d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) SVO_FAIL(SVO_EINVAL, "svo_cast_wire: no diagnostics (svo_cast_rays has them)");
+    WireParams Q;
+    int rc = wire_params(t, d, "svo_cast_wire", Q);  // (the wire formats' limits)
+    if (rc) return rc;
+    const svo_hits o = {nullptr, nullptr, nullptr, ao};
+    return cast_launch(t, d, &o, wire, stream);
+}
+
+static int cast_launch(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, void* wire, void* stream) {
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_rays: tree not uploaded (svo_upload)");
     if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: castRayFromCam semantics need a solid-view tree");
     if (d->steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: negative step budget");
@@ -1885,6 +1840,8 @@ extern "C" int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const sv
     int64_t n = 0;
     int rc = fill_params(t, d, o, P, n);
     if (rc) return rc;
+    P.wire = reinterpret_cast<uint32_t*>(wire);
+    P.wire_compact = wire && wire_bytes_for(t, d) == 8;
     if (n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
@@ -1961,70 +1918,25 @@ extern "C" int svo_sync(void* stream) {
 }
 
 // ================================================================================================
-// wire format of hit records for the tile-row gather (include/svo_rt.h: 12 B per ray)
+// wire records of the tile-row gather (svo_wire.h: 8 B compact, 12 B general)
 // ================================================================================================
-namespace {
-
-struct WireParams {
-    int64_t n, frame_records;
-    int32_t explicit_mode, steps;
-    float frame_org[3 * SVO_MAX_FRAMES];
-    const float* rorg;  // explicit rays: per-ray origins (or null: frame_org[0..2])
-    int32_t* pos;
-    float* t;
-    uint32_t* info;
-    uint32_t* wire;
-};
-
-// trunc of the origin the record's ray started from (dda_axis: round = trunc(origin))
-__device__ __forceinline__ void record_origin_cell(const WireParams& Q, int64_t i, int32_t c[3]) {
-    if (Q.explicit_mode && Q.rorg) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) c[k] = (int32_t)__builtin_truncf(Q.rorg[3 * i + k]);
-    } else {
-        const int64_t f = Q.explicit_mode ? 0 : i / Q.frame_records;
-#pragma unroll
-        for (int k = 0; k < 3; k++) c[k] = (int32_t)__builtin_truncf(Q.frame_org[3 * f + k]);
-    }
+// 8-B records for frame descs from integral / half-integral camera positions (every crossing sum exact)
+int32_t svo::wire_bytes_for(const svo_tree* t, const svo_cast_desc* d) {
+    if (d->ray_dirs || d->steps > 32767 || t->palette.size() > 4096) return 12;
+    const int32_t nf = d->n_frames > 1 ? d->n_frames : 1;
+    for (int32_t f = 0; f < nf; f++)
+        for (int k = 0; k < 3; k++) {
+            const float o = nf > 1 ? d->frame_origins[3 * f + k] : d->origin[k];
+            if (!(2.0f * o == __builtin_truncf(2.0f * o) && __builtin_fabsf(o) < 1073741824.0f)) return 12;
+        }
+    return 8;
 }
 
-__global__ __launch_bounds__(256) void k_hits_pack(const WireParams Q) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= Q.n) return;
-    int32_t c[3];
-    record_origin_cell(Q, i, c);
-    const int4 ps = reinterpret_cast<const int4*>(Q.pos)[i];
-    const uint32_t inf = Q.info[i];
-    const uint32_t i16 = ((inf >> 31) << 15) | (((inf >> AXIS_SHIFT) & 3u) << 13) | (((inf & NEG_BIT) ? 1u : 0u) << 12) | (inf & 0xFFFu);
-    const uint32_t dx = (uint32_t)(ps.x - c[0]) & 0xFFFFu, dy = (uint32_t)(ps.y - c[1]) & 0xFFFFu, dz = (uint32_t)(ps.z - c[2]) & 0xFFFFu;
-    uint32_t* w = Q.wire + 3 * i;
-    w[0] = dx | (dy << 16);
-    w[1] = dz | (i16 << 16);
-    w[2] = __float_as_uint(Q.t[i]);
-}
-
-__global__ __launch_bounds__(256) void k_hits_unpack(const WireParams Q) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= Q.n) return;
-    int32_t c[3];
-    record_origin_cell(Q, i, c);
-    const uint32_t* w = Q.wire + 3 * i;
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const int32_t dx = (int32_t)(int16_t)(w0 & 0xFFFFu), dy = (int32_t)(int16_t)(w0 >> 16), dz = (int32_t)(int16_t)(w1 & 0xFFFFu);
-    const uint32_t i16 = w1 >> 16;
-    const bool hit = (i16 >> 15) != 0u;
-    // one voxel per DDA step on one axis: a hit used |dx| + |dy| + |dz| steps, a miss all of them
-    const int32_t left = hit ? Q.steps - (abs(dx) + abs(dy) + abs(dz)) : 0;
-    reinterpret_cast<int4*>(Q.pos)[i] = make_int4(c[0] + dx, c[1] + dy, c[2] + dz, left);
-    Q.t[i] = __uint_as_float(w2);
-    Q.info[i] = (hit ? HIT_BIT : 0u) | (((i16 >> 13) & 3u) << AXIS_SHIFT) | (((i16 >> 12) & 1u) ? NEG_BIT : 0u) | (i16 & 0xFFFu);
-}
-
-int wire_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* h, const char* fn, WireParams& Q) {
-    if (!t || !d || !h || !h->pos_steps || !h->t || !h->info) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL argument");
+int svo::wire_params(const svo_tree* t, const svo_cast_desc* d, const char* fn, WireParams& Q) {
+    if (!t || !d) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL argument");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, std::string(fn) + ": tree not uploaded (svo_upload)");
-    if (d->steps < 0 || d->steps > 32767) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire format needs steps <= 32767");
-    if (t->palette.size() > 4096) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire format needs fewer than 4096 materials");
+    if (d->steps < 0 || d->steps > 32767) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire formats need steps <= 32767");
+    if (t->palette.size() > 4096) SVO_FAIL(SVO_ERANGE, std::string(fn) + ": the wire formats need at most 4096 materials");
     memset(&Q, 0, sizeof(Q));
     int64_t n = 0;
     int rc = svo_cast_count(d, &n);
@@ -2033,24 +1945,61 @@ int wire_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* h, co
     Q.n = n;
     Q.steps = d->steps;
     Q.explicit_mode = d->ray_dirs != nullptr;
+    Q.compact = wire_bytes_for(t, d) == 8;
     const int32_t nf = (!Q.explicit_mode && d->n_frames > 1) ? d->n_frames : 1;
-    Q.frame_records = n / nf;
+    Q.frame_records = std::max<int64_t>(1, n / nf);
     for (int32_t f = 0; f < nf; f++)
         for (int k = 0; k < 3; k++) Q.frame_org[3 * f + k] = nf > 1 ? d->frame_origins[3 * f + k] : d->origin[k];
     Q.rorg = Q.explicit_mode ? d->ray_origins : nullptr;
-    Q.pos = h->pos_steps;
-    Q.t = h->t;
-    Q.info = h->info;
+    if (!Q.explicit_mode) {
+        raygen_init(Q.rg, d->cam_dir, d->ppx, d->ppy, d->width, d->height);
+        Q.width = d->width;
+        Q.tile_row_start = d->tile_row_start;
+        Q.tile_row_step = d->tile_row_step;
+        Q.frame_pixels = (int64_t)d->width * d->height;
+    }
+    return SVO_OK;
+}
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_hits_pack(const WireParams Q) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= Q.n) return;
+    float o[3];
+    wire_origin(Q, i, o);
+    const int4 ps = reinterpret_cast<const int4*>(Q.pos)[i];
+    wire_put(Q.wire, Q.compact != 0, i, o, ps.x, ps.y, ps.z, Q.t[i], Q.info[i]);
+}
+
+__global__ __launch_bounds__(256) void k_hits_unpack(const WireParams Q) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= Q.n) return;
+    wire_get(Q, i);
+}
+
+int hits_check(const svo_hits* h, const char* fn) {
+    if (!h || !h->pos_steps || !h->t || !h->info) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL hit buffer");
     return SVO_OK;
 }
 
 }  // namespace
 
+extern "C" int svo_wire_bytes(const svo_tree* t, const svo_cast_desc* d, int32_t* bytes) {
+    if (!t || !d || !bytes) SVO_FAIL(SVO_EINVAL, "svo_wire_bytes: NULL argument");
+    *bytes = wire_bytes_for(t, d);
+    return SVO_OK;
+}
+
 extern "C" int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const svo_hits* hits, void* wire, void* stream) {
     WireParams Q;
-    int rc = wire_params(t, d, hits, "svo_hits_pack", Q);
+    int rc = wire_params(t, d, "svo_hits_pack", Q);
+    if (!rc) rc = hits_check(hits, "svo_hits_pack");
     if (rc) return rc;
     if (!wire) SVO_FAIL(SVO_EINVAL, "svo_hits_pack: NULL wire buffer");
+    Q.pos = hits->pos_steps;
+    Q.t = hits->t;
+    Q.info = hits->info;
     Q.wire = reinterpret_cast<uint32_t*>(wire);
     if (Q.n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
@@ -2059,15 +2008,35 @@ extern "C" int svo_hits_pack(const svo_tree* t, const svo_cast_desc* d, const sv
     return SVO_OK;
 }
 
-extern "C" int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* stream) {
+// unpack into record order (scatter = 0) or into the whole frames at pixel positions (scatter = 1)
+static int wire_decode(const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao, const svo_hits* hits, void* stream,
+                       int32_t scatter, const char* fn) {
     WireParams Q;
-    int rc = wire_params(t, d, hits, "svo_hits_unpack", Q);
+    int rc = wire_params(t, d, fn, Q);
+    if (!rc) rc = hits_check(hits, fn);
     if (rc) return rc;
-    if (!wire) SVO_FAIL(SVO_EINVAL, "svo_hits_unpack: NULL wire buffer");
+    if (!wire) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL wire buffer");
+    if (scatter && Q.explicit_mode) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": explicit rays have no pixels to scatter to");
+    if (ao && !hits->ao) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": AO counts without an ao buffer");
     Q.wire = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(wire));
+    Q.pos = hits->pos_steps;
+    Q.t = hits->t;
+    Q.info = hits->info;
+    Q.ao_in = ao;
+    Q.ao_out = ao ? hits->ao : nullptr;
+    Q.scatter = scatter;
     if (Q.n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     hipLaunchKernelGGL(k_hits_unpack, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Q);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
+}
+
+extern "C" int svo_hits_unpack(const svo_tree* t, const svo_cast_desc* d, const void* wire, const svo_hits* hits, void* stream) {
+    return wire_decode(t, d, wire, nullptr, hits, stream, 0, "svo_hits_unpack");
+}
+
+extern "C" int svo_wire_scatter(const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao, const svo_hits* frames,
+                                void* stream) {
+    return wire_decode(t, d, wire, ao, frames, stream, 1, "svo_wire_scatter");
 }

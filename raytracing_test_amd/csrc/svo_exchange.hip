@@ -7,9 +7,11 @@
 // Transport: RCCL point-to-point inside one group (ncclGroupStart / ncclSend / ncclRecv /
 // ncclGroupEnd) — one frame to one rank is a gather, N frames to N ranks an all-to-all, and either is
 // one group call whose traffic spreads over every rank's links (xGMI is point to point: a gather of
-// N frames into rank 0 would put all of it on rank 0's links).  Records travel in the 12-B wire format
-// of svo_hits_pack (+1 B of AO count).  The local shard goes through RCCL as well (a send to self), so
-// a single-rank exchange runs the whole path.
+// N frames into rank 0 would put all of it on rank 0's links).  Records travel in the wire formats of
+// svo_wire.h — 8 B for frames from integral / half-integral camera positions, else 12 B — (+1 B of AO
+// count).  The local shard never travels: the display rank decodes it straight from its own wire buffer.
+// svo_exchange_wire takes the wire records the cast kernel wrote itself (svo_cast_wire: no hit records,
+// no pack pass); svo_exchange_frames packs given hit records first.
 //
 // RCCL is bound at run time (dlopen "librccl.so.1"): inside a process that already holds an RCCL
 // (e.g. torch's), that library instance is reused, so communicators the caller made there can be
@@ -28,6 +30,7 @@
 #include "../../include/svo_rt.h"
 #include "svo_hip.h"
 #include "svo_internal.h"
+#include "svo_wire.h"
 
 using namespace svo;
 
@@ -41,6 +44,7 @@ struct Rccl {
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
     ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
+    ncclResult_t (*CommCuDevice)(const ncclComm_t, int*) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
     ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -70,6 +74,7 @@ Rccl& rccl() {
         sym(R.CommDestroy, "ncclCommDestroy");
         sym(R.CommCount, "ncclCommCount");
         sym(R.CommUserRank, "ncclCommUserRank");
+        sym(R.CommCuDevice, "ncclCommCuDevice");
         sym(R.GroupStart, "ncclGroupStart");
         sym(R.GroupEnd, "ncclGroupEnd");
         sym(R.Send, "ncclSend");
@@ -86,37 +91,11 @@ Rccl& rccl() {
         if (r_ != ncclSuccess) SVO_FAIL(SVO_EDEVICE, std::string(#expr " failed: ") + rccl().GetErrorString(r_)); \
     } while (0)
 
-// One shard's wire records (and AO counts) -> their pixels of a whole frame.  Shard record i (rank r
-// of N, local row lr = i / W, column px = i % W) is pixel row (r + (lr / 8) * N) * 8 + lr % 8.
-struct ScatterParams {
-    const uint32_t* wire;
-    const uint8_t* ao_in;
-    int64_t n;
-    int32_t width, rank, nranks, steps;
-    int32_t cell[3];  // trunc(frame origin)
-    int32_t* pos;
-    float* t;
-    uint32_t* info;
-    uint8_t* ao_out;
-};
-
-__global__ __launch_bounds__(256) void k_scatter_unpack(const ScatterParams Q) {
+// One source shard's wire records (and AO counts) -> their pixels of the whole frames (svo_wire.h)
+__global__ __launch_bounds__(256) void k_wire_scatter(const WireParams Q) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= Q.n) return;
-    const int64_t lr = i / Q.width, px = i - lr * Q.width;
-    const int64_t py = ((int64_t)Q.rank + (lr >> 3) * Q.nranks) * 8 + (lr & 7);
-    const int64_t o = py * Q.width + px;
-    const uint32_t* w = Q.wire + 3 * i;
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const int32_t dx = (int32_t)(int16_t)(w0 & 0xFFFFu), dy = (int32_t)(int16_t)(w0 >> 16), dz = (int32_t)(int16_t)(w1 & 0xFFFFu);
-    const uint32_t i16 = w1 >> 16;
-    const bool hit = (i16 >> 15) != 0u;
-    // (svo_hits_unpack's reconstruction: one voxel per DDA step on one axis)
-    const int32_t left = hit ? Q.steps - (abs(dx) + abs(dy) + abs(dz)) : 0;
-    reinterpret_cast<int4*>(Q.pos)[o] = make_int4(Q.cell[0] + dx, Q.cell[1] + dy, Q.cell[2] + dz, left);
-    Q.t[o] = __uint_as_float(w2);
-    Q.info[o] = (hit ? HIT_BIT : 0u) | (((i16 >> 13) & 3u) << AXIS_SHIFT) | (((i16 >> 12) & 1u) ? NEG_BIT : 0u) | (i16 & 0xFFFu);
-    if (Q.ao_out) Q.ao_out[o] = Q.ao_in[i];
+    wire_get(Q, i);
 }
 
 // records of one frame in the shard of `rank` (svo_cast_count's rows x width)
@@ -192,6 +171,9 @@ extern "C" int svo_exchange_wrap(void* nccl_comm, int32_t device, svo_exchange**
     int n = 0, r = 0;
     NCCL_TRY(R.CommCount((ncclComm_t)nccl_comm, &n));
     NCCL_TRY(R.CommUserRank((ncclComm_t)nccl_comm, &r));
+    int cdev = -1;
+    NCCL_TRY(R.CommCuDevice((ncclComm_t)nccl_comm, &cdev));
+    if (cdev != device) SVO_FAIL(SVO_EINVAL, "svo_exchange_wrap: the communicator is on another device");
     svo_exchange* x = new (std::nothrow) svo_exchange();
     if (!x) SVO_FAIL(SVO_ENOMEM, "svo_exchange_wrap: out of memory");
     x->comm = (ncclComm_t)nccl_comm;
@@ -218,19 +200,16 @@ extern "C" int svo_exchange_info(const svo_exchange* x, int32_t* rank, int32_t* 
     return SVO_OK;
 }
 
-extern "C" int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const svo_hits* mine,
-                                   const svo_hits* frames_out, void* stream) {
-    if (!x || !t || !d || !mine) SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: NULL argument");
-    if (d->ray_dirs) SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: frame-mode descs only");
-    if (d->tile_row_start != x->rank || d->tile_row_step != x->nranks)
-        SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: desc is not this rank's shard (tile_row_start = rank, tile_row_step = nranks)");
+// one step's exchange from `wire` (this rank's records of every frame of d, frame-major, in d's wire format;
+// frame f's at f * n_mine records)
+static int exchange_wire(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao_mine,
+                         const svo_hits* frames_out, hipStream_t st, const char* fn) {
     const int32_t nf = d->n_frames > 1 ? d->n_frames : 1;
     const int32_t N = x->nranks, me = x->rank;
     const bool ao = d->ao_samples > 0;
-    if (ao && !mine->ao) SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: AO counts requested without an ao buffer");
     const int32_t n_own = nf > me ? (nf - me + N - 1) / N : 0;  // frames me, me + N, ...
     if (n_own > 0 && (!frames_out || !frames_out->pos_steps || !frames_out->t || !frames_out->info || (ao && !frames_out->ao)))
-        SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: this rank displays frames but frames_out is incomplete");
+        SVO_FAIL(SVO_EINVAL, std::string(fn) + ": this rank displays frames but frames_out is incomplete");
     const int64_t frame = (int64_t)d->width * d->height;
     std::vector<int64_t> cnt(N), off(N + 1, 0);
     for (int32_t r = 0; r < N; r++) {
@@ -238,56 +217,99 @@ extern "C" int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo
         off[r + 1] = off[r] + cnt[r];
     }
     const int64_t n_mine = cnt[me];
-    HIP_TRY(hipSetDevice(x->device), SVO_EDEVICE);
-    hipStream_t st = (hipStream_t)stream;
-    // my records of every frame, packed: frame f's at f * n_mine
-    int rc = grow(&x->send, &x->send_bytes, std::max<size_t>(16, (size_t)(n_mine * nf) * SVO_WIRE_BYTES));
-    if (!rc) rc = grow(&x->recv, &x->recv_bytes, std::max<size_t>(16, (size_t)(n_own * frame) * (SVO_WIRE_BYTES + (ao ? 1 : 0))));
+    WireParams Q0;
+    int rc = wire_params(t, d, fn, Q0);
     if (rc) return rc;
-    rc = svo_hits_pack(t, d, mine, x->send, stream);
+    const size_t wb = Q0.compact ? 8 : 12;
+    // the records of my frames from every other rank (their shard of frame k at k * frame + off[r])
+    rc = grow(&x->recv, &x->recv_bytes, std::max<size_t>(16, (size_t)(n_own * frame) * (wb + (ao ? 1 : 0))));
     if (rc) return rc;
-    uint8_t* sw = reinterpret_cast<uint8_t*>(x->send);
+    const uint8_t* sw = reinterpret_cast<const uint8_t*>(wire);
     uint8_t* rw = reinterpret_cast<uint8_t*>(x->recv);
-    uint8_t* rao = rw + (size_t)(n_own * frame) * SVO_WIRE_BYTES;  // AO counts after the records
-    Rccl& R = rccl();
-    NCCL_TRY(R.GroupStart());
-    for (int32_t f = 0; f < nf && n_mine > 0; f++) {
-        const int32_t owner = f % N;
-        NCCL_TRY(R.Send(sw + (size_t)(f * n_mine) * SVO_WIRE_BYTES, (size_t)n_mine * SVO_WIRE_BYTES, ncclUint8, owner, x->comm, st));
-        if (ao) NCCL_TRY(R.Send(mine->ao + (size_t)(f * n_mine), (size_t)n_mine, ncclUint8, owner, x->comm, st));
-    }
-    for (int32_t k = 0; k < n_own; k++)
-        for (int32_t r = 0; r < N; r++) {
-            if (cnt[r] == 0) continue;
-            const size_t base = (size_t)(k * frame + off[r]);
-            NCCL_TRY(R.Recv(rw + base * SVO_WIRE_BYTES, (size_t)cnt[r] * SVO_WIRE_BYTES, ncclUint8, r, x->comm, st));
-            if (ao) NCCL_TRY(R.Recv(rao + base, (size_t)cnt[r], ncclUint8, r, x->comm, st));
+    uint8_t* rao = rw + (size_t)(n_own * frame) * wb;  // AO counts after the records
+    if (N > 1) {
+        Rccl& R = rccl();
+        NCCL_TRY(R.GroupStart());
+        for (int32_t f = 0; f < nf && n_mine > 0; f++) {
+            const int32_t owner = f % N;
+            if (owner == me) continue;  // (decoded from the wire buffer below)
+            NCCL_TRY(R.Send(sw + (size_t)(f * n_mine) * wb, (size_t)n_mine * wb, ncclUint8, owner, x->comm, st));
+            if (ao) NCCL_TRY(R.Send(ao_mine + (size_t)(f * n_mine), (size_t)n_mine, ncclUint8, owner, x->comm, st));
         }
-    NCCL_TRY(R.GroupEnd());
-    // unpack every received shard into its pixels of the frame
+        for (int32_t k = 0; k < n_own; k++)
+            for (int32_t r = 0; r < N; r++) {
+                if (cnt[r] == 0 || r == me) continue;
+                const size_t base = (size_t)(k * frame + off[r]);
+                NCCL_TRY(R.Recv(rw + base * wb, (size_t)cnt[r] * wb, ncclUint8, r, x->comm, st));
+                if (ao) NCCL_TRY(R.Recv(rao + base, (size_t)cnt[r], ncclUint8, r, x->comm, st));
+            }
+        NCCL_TRY(R.GroupEnd());
+    }
+    // decode every shard of my frames into its pixels (my own shard straight from the wire buffer)
     for (int32_t k = 0; k < n_own; k++) {
         const int32_t f = me + k * N;
         const float* org = nf > 1 ? d->frame_origins + 3 * f : d->origin;
         for (int32_t r = 0; r < N; r++) {
             if (cnt[r] == 0) continue;
-            ScatterParams Q;
-            memset(&Q, 0, sizeof(Q));
+            WireParams Q = Q0;
             const size_t base = (size_t)(k * frame + off[r]);
-            Q.wire = reinterpret_cast<const uint32_t*>(rw + base * SVO_WIRE_BYTES);
-            Q.ao_in = ao ? rao + base : nullptr;
+            if (r == me) {
+                Q.wire = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(sw + (size_t)(f * n_mine) * wb));
+                Q.ao_in = ao ? ao_mine + (size_t)(f * n_mine) : nullptr;
+            } else {
+                Q.wire = reinterpret_cast<uint32_t*>(rw + base * wb);
+                Q.ao_in = ao ? rao + base : nullptr;
+            }
             Q.n = cnt[r];
-            Q.width = d->width;
-            Q.rank = r;
-            Q.nranks = N;
-            Q.steps = d->steps;
-            for (int a = 0; a < 3; a++) Q.cell[a] = (int32_t)truncf(org[a]);
+            Q.frame_records = cnt[r];
+            Q.tile_row_start = r;
+            Q.tile_row_step = N;
+            Q.scatter = 1;
+            Q.frame_pixels = frame;
+            for (int a = 0; a < 3; a++) Q.frame_org[a] = org[a];
             Q.pos = frames_out->pos_steps + 4 * (size_t)(k * frame);
             Q.t = frames_out->t + (size_t)(k * frame);
             Q.info = frames_out->info + (size_t)(k * frame);
             Q.ao_out = ao ? frames_out->ao + (size_t)(k * frame) : nullptr;
-            hipLaunchKernelGGL(k_scatter_unpack, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, st, Q);
+            hipLaunchKernelGGL(k_wire_scatter, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, st, Q);
             HIP_TRY(hipGetLastError(), SVO_EDEVICE);
         }
     }
     return SVO_OK;
+}
+
+static int exchange_check(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const char* fn) {
+    if (!x || !t || !d) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": NULL argument");
+    if (d->ray_dirs) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": frame-mode descs only");
+    if (d->tile_row_start != x->rank || d->tile_row_step != x->nranks)
+        SVO_FAIL(SVO_EINVAL, std::string(fn) + ": desc is not this rank's shard (tile_row_start = rank, tile_row_step = nranks)");
+    if (t->device != x->device) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": the tree lives on another device than the exchange");
+    HIP_TRY(hipSetDevice(x->device), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+extern "C" int svo_exchange_wire(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const void* wire, const uint8_t* ao,
+                                 const svo_hits* frames_out, void* stream) {
+    int rc = exchange_check(x, t, d, "svo_exchange_wire");
+    if (rc) return rc;
+    if (!wire) SVO_FAIL(SVO_EINVAL, "svo_exchange_wire: NULL wire buffer");
+    if (d->ao_samples > 0 && !ao) SVO_FAIL(SVO_EINVAL, "svo_exchange_wire: AO counts requested without an ao buffer");
+    return exchange_wire(x, t, d, wire, ao, frames_out, (hipStream_t)stream, "svo_exchange_wire");
+}
+
+extern "C" int svo_exchange_frames(svo_exchange* x, const svo_tree* t, const svo_cast_desc* d, const svo_hits* mine,
+                                   const svo_hits* frames_out, void* stream) {
+    int rc = exchange_check(x, t, d, "svo_exchange_frames");
+    if (rc) return rc;
+    if (!mine) SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: NULL argument");
+    if (d->ao_samples > 0 && !mine->ao) SVO_FAIL(SVO_EINVAL, "svo_exchange_frames: AO counts requested without an ao buffer");
+    const int32_t nf = d->n_frames > 1 ? d->n_frames : 1;
+    const int64_t n_mine = shard_records(d->width, d->height, x->rank, x->nranks);
+    // my records of every frame, packed (frame f's at f * n_mine)
+    rc = grow(&x->send, &x->send_bytes, std::max<size_t>(16, (size_t)(n_mine * nf) * 12));
+    if (rc) return rc;
+    rc = svo_hits_pack(t, d, mine, x->send, stream);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(x->device), SVO_EDEVICE);  // (svo_hits_pack selected the tree's device: the same one)
+    return exchange_wire(x, t, d, x->send, mine->ao, frames_out, (hipStream_t)stream, "svo_exchange_frames");
 }

@@ -22,8 +22,11 @@ def _free_port():
 def _records(ref, pixel_idx):
     import torch
 
-    info = (ref["hit"][pixel_idx].astype(np.uint32) << 31) | (ref["axis"][pixel_idx].astype(np.uint32) & 3) << 16
-    info |= (ref["flags"][pixel_idx] & 0xFFFF).astype(np.uint32)
+    axis = ref["axis"][pixel_idx]
+    step = ref["pos"][pixel_idx] - ref["last"][pixel_idx]  # the last step (one axis, +-1)
+    neg = (axis < 3) & (step[np.arange(len(axis)), np.minimum(axis, 2)] < 0)
+    info = (ref["hit"][pixel_idx].astype(np.uint32) << 31) | (axis.astype(np.uint32) & 3) << 16 | (neg.astype(np.uint32) << 18)
+    info |= (ref["flags"][pixel_idx] & 0xFFF).astype(np.uint32)
     ps = np.concatenate([ref["pos"][pixel_idx], ref["steps"][pixel_idx, None]], 1).astype(np.int32)
     return {"pos_steps": torch.from_numpy(ps), "t": torch.from_numpy(ref["t"][pixel_idx].astype(np.float32)),
             "info": torch.from_numpy(info.view(np.int32))}
@@ -77,7 +80,7 @@ def test_tile_row_shard_gather_reassemble(world):
         assert np.array_equal(full[k], want[k].numpy()), k
 
 
-def _wire_worker(rank, world, port, W, H, origins, q, all_to_all=False):
+def _wire_worker(rank, world, port, W, H, origins, q, all_to_all=False, compact=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
@@ -99,12 +102,16 @@ def _wire_worker(rank, world, port, W, H, origins, q, all_to_all=False):
         ref = T.cast_frame(org, cam, W, H, 300, pixels=pix, nthreads=2)
         r = _records(ref, np.arange(len(pix)))
         cell = np.trunc(np.asarray(org, np.float32)).astype(np.int32)
-        parts.append(wire_ref.pack(r["pos_steps"].numpy(), r["t"].numpy(), r["info"].numpy().view(np.uint32), cell[None, :]))
+        if compact:
+            parts.append(wire_ref.pack_compact(r["pos_steps"].numpy(), r["info"].numpy().view(np.uint32), cell[None, :]))
+        else:
+            parts.append(wire_ref.pack(r["pos_steps"].numpy(), r["t"].numpy(), r["info"].numpy().view(np.uint32), cell[None, :]))
     mine = np.concatenate(parts)
+    wb = mine.shape[1]
     if all_to_all:
         # frame f displayed by rank f (frames = ranks): my rows of frame f go to rank f
         counts = [shard.shard_count(W, H, r, world) for r in range(world)]
-        recv = torch.zeros((W * H, 12), dtype=torch.uint8)
+        recv = torch.zeros((W * H, wb), dtype=torch.uint8)
         dist.all_to_all_single(recv, torch.from_numpy(mine), output_split_sizes=counts, input_split_sizes=[len(pix)] * world)
         q.put((rank, recv.numpy().copy()))
     else:
@@ -117,10 +124,12 @@ def _wire_worker(rank, world, port, W, H, origins, q, all_to_all=False):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_wire_all_to_all_frame_per_rank(world):
+def test_wire_all_to_all_frame_per_rank(world, compact):
     """bench.py's N>1 exchange: N frames per step, frame f displayed by rank f — one all-to-all of
-    12-B wire records; every rank's frame, unpacked, equals its single-rank cast."""
+    wire records (12 B, or the 8-B compact records of integral camera positions, whose receiver rebuilds
+    each pixel's ray: tests/wire_ref.py); every rank's frame, unpacked, equals its single-rank cast."""
     import multiprocessing as mp
 
     sys.path.insert(0, ROOT)
@@ -134,7 +143,7 @@ def test_wire_all_to_all_frame_per_rank(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_wire_worker, args=(r, world, port, W, H, origins, q, True)) for r in range(world)]
+    ps = [ctx.Process(target=_wire_worker, args=(r, world, port, W, H, origins, q, True, compact)) for r in range(world)]
     for p in ps:
         p.start()
     got = dict(q.get(timeout=300) for _ in range(world))
@@ -151,7 +160,13 @@ def test_wire_all_to_all_frame_per_rank(world):
         for r in range(world):
             rows = shard.shard_pixel_rows(H, r, world)
             idx = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1)
-            ps_, t_, info_ = wire_ref.unpack(got[f][offs[r]:offs[r + 1]], cell, 300)
+            if compact:
+                ppx, ppy = O.proj_plane(W, H)
+                dirs = np.array([O.pixel_dir(cam, ppx, ppy, W, H, int(i % W), int(i // W)) for i in idx], np.float32)
+                ps_, t_, info_ = wire_ref.unpack_compact(got[f][offs[r]:offs[r + 1]], np.repeat(np.asarray([org], np.float32), len(idx), 0),
+                                                         dirs, 300)
+            else:
+                ps_, t_, info_ = wire_ref.unpack(got[f][offs[r]:offs[r + 1]], cell, 300)
             assert np.array_equal(ps_, want["pos_steps"].numpy()[idx]), (f, r)
             assert np.array_equal(t_, want["t"].numpy()[idx]), (f, r)
             assert np.array_equal(info_.view(np.int32), want["info"].numpy()[idx]), (f, r)

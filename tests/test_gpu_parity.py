@@ -56,7 +56,7 @@ CAMERAS = [
     ((100.0, 120.0, 100.0), (1.0, -1.2, 0.3)),
     ((150.3, 44.7, 20.9), (-0.6, -0.2, 1.0)),   # fractional origin, negative x
     ((60.5, 70.5, 40.5), (1.0, -0.5, 0.6)),     # half-integral origins: the linear (no-segment) instance
-    ((-20.5, 55.5, 130.5), (0.7, -0.3, -1.0)),  # (negative: trunc != floor, deltaPos starts at 1.5a / -0.5a)
+    ((-20.5, 55.5, 130.5), (0.7, -0.3, 1.0)),   # (negative x: trunc != floor, deltaPos starts at 1.5a / -0.5a)
 ]
 
 
@@ -282,10 +282,12 @@ def test_multi_frame_launch(rt, torch_cuda, gtree):
                 assert np.array_equal(multi[k][f * per:(f + 1) * per], one[k]), (start, step, f, k)
 
 
-def test_wire_pack_roundtrip(rt, torch_cuda, gtree):
-    """svo_hits_pack / svo_hits_unpack (the exchange format of the tile-row gather) against the
-    numpy restatement in tests/wire_ref.py, and unpack(pack(records)) == records: hits and misses
-    (budget 30), several frames, explicit rays with their own origins."""
+def test_wire_formats(rt, torch_cuda, gtree):
+    """svo_hits_pack / svo_hits_unpack / svo_cast_wire (the exchange formats of the tile-row gather) against
+    the numpy restatements in tests/wire_ref.py, and unpack(pack(records)) == records: 8-B compact records
+    for frames from integral / half-integral camera positions (the receiver rebuilds each pixel's ray for
+    the position and t), 12-B records for other origins and explicit rays; hits and misses (budget 30),
+    several frames, axis-aligned camera directions (exact zero components: NaN / infinite deltaPos)."""
     import os
     import sys
 
@@ -293,26 +295,42 @@ def test_wire_pack_roundtrip(rt, torch_cuda, gtree):
     import wire_ref
 
     torch = torch_cuda
-    _, d = CAMERAS[0]
-    dn = rt.normalize(d)
-    origins = [(35.0, 50.0, 35.0), (-3.5, 40.25, -2.75), (1020.5, 35.5, 50.5)]
-    for steps in (30, 300):
-        desc = rt.Tree.frame_desc(origins[0], dn, 64, 40, steps, frame_origins=origins)
-        n = rt.Tree.count(desc)
-        out = rt.Tree.alloc_hits(n, 0)
-        gtree.cast(desc, out)
-        wire = torch.zeros((n, rt.WIRE_BYTES), dtype=torch.uint8, device="cuda")
-        gtree.pack_hits(desc, out, wire)
-        back = rt.Tree.alloc_hits(n, 0)
-        gtree.unpack_hits(desc, wire, back)
-        torch.cuda.synchronize()
-        cells = np.repeat(np.trunc(np.asarray(origins, np.float32)).astype(np.int32), n // len(origins), 0)
-        ps, t, info = out["pos_steps"].cpu().numpy(), out["t"].cpu().numpy(), out["info"].cpu().numpy().view(np.uint32)
-        assert np.array_equal(wire.cpu().numpy(), wire_ref.pack(ps, t, info, cells)), steps
-        for k in ("pos_steps", "t", "info"):
-            assert np.array_equal(back[k].cpu().numpy(), out[k].cpu().numpy()), (steps, k)
-        g = rt.decode_hits(out)
-        assert 0 < g["hit"].sum() < n or steps == 300  # both kinds of records at the small budget
+    cases = [([(35.0, 50.0, 35.0), (-3.5, 40.25, -2.75), (1020.5, 35.5, 50.5)], (1.0, 0.0, 1.0), 12),
+             ([(35.0, 50.0, 35.0), (-3.5, 40.5, -2.0), (1020.5, 35.5, 50.5)], (1.0, 0.0, 1.0), 8),
+             ([(4.0, 90.0, 4.0), (60.5, 70.5, 40.5)], (1.0, -0.45, 1.0), 8),
+             ([(50.5, 60.0, 50.5)], (0.0, -1.0, 0.0), 8), ([(100.0, 80.0, 20.0)], (-0.3, -0.4, 1.0), 8)]
+    for origins, cam, wb in cases:
+        dn = rt.normalize(cam)
+        for steps in (30, 300):
+            desc = rt.Tree.frame_desc(origins[0], dn, 64, 40, steps, frame_origins=origins if len(origins) > 1 else None)
+            assert gtree.wire_bytes(desc) == wb, (origins, wb)
+            n = rt.Tree.count(desc)
+            out = rt.Tree.alloc_hits(n, 0)
+            gtree.cast(desc, out)
+            wire = torch.zeros((n, wb), dtype=torch.uint8, device="cuda")
+            gtree.pack_hits(desc, out, wire)
+            fused = torch.zeros((n, wb), dtype=torch.uint8, device="cuda")
+            gtree.cast_wire(desc, fused)
+            back = rt.Tree.alloc_hits(n, 0)
+            gtree.unpack_hits(desc, wire, back)
+            torch.cuda.synchronize()
+            assert torch.equal(fused, wire), (origins, steps)  # the cast kernel's own wire records == pack(cast)
+            per = n // len(origins)
+            o = np.repeat(np.asarray(origins, np.float32), per, 0)
+            cells = np.trunc(o).astype(np.int32)
+            ps, t, info = out["pos_steps"].cpu().numpy(), out["t"].cpu().numpy(), out["info"].cpu().numpy().view(np.uint32)
+            w = wire.cpu().numpy()
+            if wb == 12:
+                assert np.array_equal(w, wire_ref.pack(ps, t, info, cells)), steps
+            else:
+                assert np.array_equal(w, wire_ref.pack_compact(ps, info, cells)), steps
+                dirs = np.tile(rt.pixel_dirs(dn, 64, 40).reshape(-1, 3), (len(origins), 1))
+                ps2, t2, info2 = wire_ref.unpack_compact(w, o, dirs, steps)
+                assert np.array_equal(ps2, ps) and np.array_equal(info2, info) and np.array_equal(t2.view(np.uint32), t.view(np.uint32))
+            for k in ("pos_steps", "t", "info"):
+                assert np.array_equal(back[k].cpu().numpy().view(np.uint32), out[k].cpu().numpy().view(np.uint32)), (origins, steps, k)
+            g = rt.decode_hits(out)
+            assert 0 < g["hit"].sum() < n or steps == 300  # both kinds of records at the small budget
     rng = np.random.default_rng(3)
     org = np.stack([rng.uniform(-50, 250, 500), rng.uniform(0, 120, 500), rng.uniform(-50, 250, 500)], 1).astype(np.float32)
     dr = rng.normal(size=(500, 3)).astype(np.float32)
@@ -321,13 +339,44 @@ def test_wire_pack_roundtrip(rt, torch_cuda, gtree):
     out = gtree.cast_rays(gd, go, steps=300)
     desc = rt.CastDesc()
     desc.ray_dirs, desc.ray_origins, desc.n_rays, desc.steps = gd.data_ptr(), go.data_ptr(), 500, 300
-    wire = torch.zeros((500, rt.WIRE_BYTES), dtype=torch.uint8, device="cuda")
+    assert gtree.wire_bytes(desc) == 12
+    wire = torch.zeros((500, 12), dtype=torch.uint8, device="cuda")
     gtree.pack_hits(desc, out, wire)
     back = rt.Tree.alloc_hits(500, 0)
     gtree.unpack_hits(desc, wire, back)
     torch.cuda.synchronize()
     for k in ("pos_steps", "t", "info"):
         assert np.array_equal(back[k].cpu().numpy(), out[k].cpu().numpy()), k
+
+
+@pytest.mark.parametrize("N", [2, 3])
+def test_wire_scatter_shards(rt, torch_cuda, gtree, N):
+    """The display side of the N > 1 exchange on one GPU: every rank's shard (tile rows r, r + N, ... of two
+    frames, a height that is not a multiple of 8) cast straight to wire records (svo_cast_wire) and decoded
+    into its pixels of the whole frames (svo_wire_scatter, the exchange's decode): the union equals one
+    unsharded cast of each frame, in both wire formats, AO counts alongside."""
+    torch = torch_cuda
+    cam = rt.normalize((1.0, -0.45, 1.0))
+    W, H = 50, 37
+    for origins in ([(4.0, 90.0, 4.0), (60.5, 70.5, 40.5)], [(4.25, 90.0, 4.0), (60.5, 70.5, 40.5)]):
+        frames = rt.Tree.alloc_hits(2 * W * H, 0, ao=True)
+        for k in frames:
+            frames[k].fill_(-1 if frames[k].dtype != torch.uint8 else 255)
+        for r in range(N):
+            d = rt.Tree.frame_desc(origins[0], cam, W, H, 300, tile_row_start=r, tile_row_step=N, frame_origins=origins, ao_samples=16)
+            n = rt.Tree.count(d)
+            wb = gtree.wire_bytes(d)
+            assert wb == (8 if origins[0][0] == 4.0 else 12)
+            wire = torch.zeros((n, wb), dtype=torch.uint8, device="cuda")
+            ao = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            gtree.cast_wire(d, wire, ao)
+            gtree.wire_scatter(d, wire, frames, ao=ao)
+        torch.cuda.synchronize()
+        for f, org in enumerate(origins):
+            one = gtree.cast_frame(org, cam, W, H, 300, ao_samples=16)
+            for k in ("pos_steps", "t", "info", "ao"):
+                got = frames[k][f * W * H:(f + 1) * W * H]
+                assert torch.equal(got, one[k]), (N, origins, f, k)
 
 
 def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):
@@ -598,6 +647,15 @@ def test_exchange_single_rank_python(rt, gtree, torch_cuda):
             torch.cuda.synchronize()
             for k in mine:
                 assert torch.equal(out[k], mine[k]), (nf, k)
+            # the fused path: the cast writes wire records, the exchange decodes them
+            wire = torch.zeros((n, gtree.wire_bytes(d)), dtype=torch.uint8, device="cuda")
+            wao = torch.zeros(n, dtype=torch.uint8, device="cuda") if ao else None
+            gtree.cast_wire(d, wire, wao)
+            out2 = rt.Tree.alloc_hits(n, 0, ao=ao > 0)
+            x.wire(gtree, d, wire, out2, ao=wao)
+            torch.cuda.synchronize()
+            for k in mine:
+                assert torch.equal(out2[k], mine[k]), (nf, k, "wire")
     finally:
         x.close()
 

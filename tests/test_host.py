@@ -20,7 +20,7 @@ def test_abi_exports_every_declared_symbol(rt):
     L = C.CDLL(rt.LIB_PATH)
     for s in declared:
         assert hasattr(L, s), s
-    assert rt.lib().svo_version() == 6
+    assert rt.lib().svo_version() == 7
 
 
 def test_product_noise_matches_reference_golden(rt):

@@ -63,6 +63,20 @@ def main():
     res["unpack_full_us"] = timed(lambda: tree.unpack_hits(full, wf, back, s))
     res["copy_wire_full_us"] = timed(lambda: wcopy.copy_(wf))
     res["exchange_1rank_us"] = timed(lambda: x.frames(tree, full, of, frames_out, s))
+    # the fused path (svo_cast_wire + svo_exchange_wire / svo_wire_scatter): wire records from the cast kernel
+    wbf, wbs = tree.wire_bytes(full), tree.wire_bytes(shard)
+    res["compact_wire_bytes"] = wbf
+    cwf = torch.empty((nf, wbf), dtype=torch.uint8, device="cuda")
+    cws = torch.empty((ns, wbs), dtype=torch.uint8, device="cuda")
+    res["cast_wire_full_us"] = timed(lambda: tree.cast_wire(full, cwf, None, s))
+    res["cast_wire_shard_us"] = timed(lambda: tree.cast_wire(shard, cws, None, s))
+    res["scatter_shard_us"] = timed(lambda: tree.wire_scatter(shard, cws, frames_out, None, s))
+    res["exchange_wire_1rank_us"] = timed(lambda: x.wire(tree, full, cwf, frames_out, None, s))
+    res["copy_compact_full_us"] = timed(lambda: cwf[: nf // 2].copy_(cwf[nf // 2: 2 * (nf // 2)]))
+    torch.cuda.synchronize()
+    tree.cast(full, of, s)
+    tree.cast_wire(full, cwf, None, s)
+    x.wire(tree, full, cwf, frames_out, None, s)
     torch.cuda.synchronize()
     ok = all(torch.equal(back[k], of[k]) for k in of) and all(torch.equal(frames_out[k], of[k]) for k in of)
     res["roundtrip_equal"] = ok
