@@ -90,6 +90,12 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+#ifndef SVO_SHADE_WAVES
+#define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
+#endif
+#ifndef SVO_XCD_GROUP
+#define SVO_XCD_GROUP 0  // A/B: footprints grouped per XCD (see k_cast)
+#endif
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -1198,7 +1204,7 @@ template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
-__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const CastParams P) {
+__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVES : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1215,6 +1221,16 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : 8) void k_cast(const Ca
         for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
     int64_t blk = blockIdx.x;
+#if SVO_XCD_GROUP > 0
+    if (P.mode == MODE_FRAME) {
+        // blocks are dealt round-robin to the 8 XCDs (b and b + 8 share an L2): within every run of
+        // 8 * G blocks, XCD x takes the G consecutive footprints x*G .. x*G + G-1, so the footprints one L2
+        // serves are neighbours (the load stays balanced: every XCD takes its share of every run)
+        constexpr int64_t G = SVO_XCD_GROUP;
+        const int64_t nb = gridDim.x, k = blk >> 3, run = k / G, base = run * 8 * G;
+        if (base + 8 * G <= nb) blk = base + (blk & 7) * G + (k - run * G);
+    }
+#endif
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
