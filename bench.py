@@ -286,15 +286,13 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
                                                                                           if world > 1 or scale != 1 else ""),
             "valu_issue_rule": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz x launch time)" % (VALU_CYCLES, N_SIMD, CLOCK_GHZ),
         })
-        sq = load_json("sq_%s.json" % run_key(args))
-        if sq:
-            q = sq["counters_per_dispatch"]
-            wc = q["SQ_WAVE_CYCLES"]
+        if all(k in c for k in ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")):
+            wc = c["SQ_WAVE_CYCLES"]
             roof["limiter"] = ("dependent instruction chains: of the wave-cycles %.0f %% issue, %.0f %% wait to issue, %.0f %% wait on "
-                               "memory (SQ counters, profiles/sq_%s.json); VALU issue %.2f of peak; measured HBM traffic %.1f %% of peak "
+                               "memory (SQ counters of the same pass); VALU issue %.2f of peak; measured HBM traffic %.1f %% of peak "
                                "(the nodes the bytes model counts are served from L2 / MALL)"
-                               % (100.0 * q["SQ_ACTIVE_INST_ANY"] / wc, 100.0 * q["SQ_WAIT_INST_ANY"] / wc, 100.0 * q["SQ_WAIT_ANY"] / wc,
-                                  run_key(args), valu_frac, 100.0 * hbm / HBM_PEAK_GBS))
+                               % (100.0 * c["SQ_ACTIVE_INST_ANY"] / wc, 100.0 * c["SQ_WAIT_INST_ANY"] / wc, 100.0 * c["SQ_WAIT_ANY"] / wc,
+                                  valu_frac, 100.0 * hbm / HBM_PEAK_GBS))
         else:
             roof["limiter"] = ("instruction stream: VALU issue %.2f of peak, measured HBM traffic %.1f %% of peak (the nodes the model "
                                "counts are served from L2 / MALL)" % (valu_frac, 100.0 * hbm / HBM_PEAK_GBS))
