@@ -241,8 +241,12 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
     model, bytes_model, extra = None, None, {}
     if not args.shade and b is not None:  # (the shading pass has no §8(d) model)
         model = b["bytes_per_ray"]
-        bytes_model = ("SURVEY.md §8d B_ray = 16 (E_child + 1) + 4 E_child + 24 B hit record, E_child = %.2f node entries per ray "
-                       "along the reference DDA path (%s, profiles/bray.json)" % (b["e_child_per_ray"], key))
+        if "e_child_per_ray" in b:
+            bytes_model = ("SURVEY.md §8d B_ray = 16 (E_child + 1) + 4 E_child + 24 B hit record, E_child = %.2f node entries per ray "
+                           "along the reference DDA path (%s, profiles/bray.json)" % (b["e_child_per_ray"], key))
+        else:  # C1: the dense grid
+            bytes_model = ("SURVEY.md §8d for the dense grid: 1 B per DDA step (%.1f per ray) + 24 B hit record (%s, profiles/bray.json)"
+                           % (b["dda_steps_per_ray"], key))
         if args.ao:
             kb = bray.get("C4_ao%d_kernel" % args.ao)
             traced = bray.get("C4_ao%d" % args.ao)
