@@ -161,6 +161,10 @@ void svo_tree_destroy(svo_tree* t);
    linearised tree (levels, view, palette, nodes, material runs; a checksum) to `path`, and read it back
    as a new tree (not uploaded).  Loading validates every child / material reference against the array
    sizes, so a damaged file fails with SVO_EIO instead of reaching a kernel. */
+/* The column ceilings the casts use (SVO_CAST_NO_CEILINGS): for k = 3 .. min(levels - 1, 6), per aligned block of
+   4^k x 4^k columns, the highest stored voxel row of the tree in those columns (-1: none), row-major [z][x],
+   level after level (finest first).  out may be NULL (count only); levels = number of levels, n = elements. */
+int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n);
 int svo_tree_save(const svo_tree* t, const char* path);
 int svo_tree_load(const char* path, svo_tree** out);
 
@@ -255,6 +259,10 @@ typedef struct {
 /* svo_cast_desc.flags (results identical): frames whose rays all step with the same signs run an
    instance with those signs compiled in; this bit keeps the per-wave sign flags instead */
 #define SVO_CAST_NO_OCTANT 16384
+/* svo_cast_desc.flags (results identical): rays above the highest stored row of the 256- or 64-column block
+   they are in cross the empty box above that row in one move, without a tree lookup (column ceilings,
+   computed at upload / sync); this bit walks the tree instead */
+#define SVO_CAST_NO_CEILINGS 32768
 
 /* number of rays a desc produces on this shard (= records written) */
 int svo_cast_count(const svo_cast_desc* d, int64_t* n);

@@ -41,11 +41,12 @@ CAST_TILE_32X2 = 512  # scheduling: one wavefront per 32x2 pixels of its 8-pixel
 CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (results identical)
 CAST_SEGMENTS = 4096  # force the kernel instance with segment-exact crossings (results identical)
 CAST_NO_OCTANT = 16384  # per-wave step-sign flags instead of the launch's compiled-in sign octant (results identical)
+CAST_NO_CEILINGS = 32768  # walk the tree instead of crossing column-ceiling boxes (results identical)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
               "no_progress", "root_starts", "cache_empty", "wave_skips", "wave_descents",
-              "path_starts", "ao_node_loads")  # wave_*: per wave (64 rays)
+              "path_starts", "ao_node_loads", "ceil_moves")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: the larger wire record (12 B general, 8 B compact: Tree.wire_bytes(desc))
@@ -138,7 +139,7 @@ ABI_SYMBOLS = (
     "svo_build_terrain_gpu", "svo_build_heightfield_gpu", "svo_hits_pack", "svo_hits_unpack", "svo_tree_node_indices",
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
-    "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire",
+    "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
 )
 
 
@@ -177,7 +178,8 @@ def lib():
                      ("svo_tree_save", [vp, C.c_char_p]), ("svo_tree_load", [C.c_char_p, C.POINTER(vp)]),
                      ("svo_wire_bytes", [vp, C.POINTER(CastDesc), C.POINTER(i32)]), ("svo_cast_wire", [vp, C.POINTER(CastDesc), vp, vp, vp]),
                      ("svo_wire_scatter", [vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
-                     ("svo_exchange_wire", [vp, vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp])):
+                     ("svo_exchange_wire", [vp, vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
+                     ("svo_tree_ceilings", [vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -550,6 +552,20 @@ class Tree:
         if ao:
             out["ao"] = torch.empty(n, dtype=torch.uint8, device=dev)
         return out
+
+    def ceilings(self):
+        """the column ceilings (svo_tree_ceilings): a list of (E / 4^k) x (E / 4^k) int16 arrays [z][x], k = 3, 4, ..."""
+        lv, n = C.c_int32(), C.c_int64()
+        _check(lib().svo_tree_ceilings(self._h, None, 0, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
+        out = np.zeros(n.value, np.int16)
+        _check(lib().svo_tree_ceilings(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
+        E = 1 << (2 * self.info().levels)
+        res, off = [], 0
+        for j in range(lv.value):
+            rows = E >> (2 * (3 + j))
+            res.append(out[off:off + rows * rows].reshape(rows, rows))
+            off += rows * rows
+        return res
 
     def wire_bytes(self, desc):
         """bytes per wire record of desc's records: 8 (compact: frames from integral / half-integral camera

@@ -87,6 +87,11 @@ struct CastParams {
     // the highest stored voxel row of the scene / of the solid tree (tree_top_y; casts: top_solid); a ray
     // moving up above it that cannot wrap in y before its budget ends can hit nothing more
     int32_t top_scene, top_solid;
+    // column ceilings of the tree the rays walk (the scene, for shading): level j's blocks are 4^(kCeilK0 + j)
+    // columns wide, row-major at ceil + ceil_off[j] (svo_internal.h tree_ceilings); ceil_levels 0: none
+    const int16_t* ceil;
+    int32_t ceil_levels;
+    int64_t ceil_off[2];
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
@@ -460,6 +465,7 @@ struct Stats {
     uint32_t path_starts;                          // lookups restarted from the LDS path
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
     uint32_t no_progress;                          // loop iterations that consumed no budget (the guard's trips: 0)
+    uint32_t ceil_moves;                           // crossings of a column-ceiling box (no lookup)
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -480,7 +486,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // Region lookup of a wrapped voxel: SOLID hit, an empty child cell (returns its shift), or the
 // brick holding the voxel (mask / ref / info returned).  tetrahexa_tree.cpp:124-152 on the
 // breadth-first layout.
-enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u };
+enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u, R_CEIL = 3u };
 
 // The interior node whose child region holds the ray's current cell, kept in registers: a move to
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
@@ -757,7 +763,8 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // walks fold away; 0: per-wave sign flags (dir_flags)
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
-template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, class Mem>
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, bool CEIL = false,
+          class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1,
@@ -830,7 +837,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -854,6 +861,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
     bool escaped = false;
+    // coordinate bits changed by ceiling moves since the last lookup (the lookup's restart depth)
+    uint32_t jump = 0u;
+    const bool ceil_on = CEIL && P.ceil_levels > 0;  // (uniform)
     while (!done) {
         // the voxel just entered is untested
         if (STATS) st.wv_iters += wave_lead();
@@ -869,8 +879,37 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const uint32_t ax = R.axis;
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
-        const uint32_t moved = wa ^ ((wa - (uint32_t)sa) & wm);  // bits the last step changed
-        const uint32_t kind = lookup<STATS, !REFLECT, KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
+        const uint32_t moved = jump | (wa ^ ((wa - (uint32_t)sa) & wm));  // bits the last step(s) changed
+        // Column ceilings: a ray above the highest stored row of the 256- (then 64-) column block it is in
+        // has only empty voxels between it and that row, and above it up to the top of the world, over the
+        // whole block: that box is crossed without a lookup (R_CEIL; the next lookup restarts from the
+        // per-lane path at the depth the moves since the last lookup left intact)
+        int32_t cex[3] = {0, 0, 0};
+        bool cl = false;
+        if (ceil_on && fast && R.steps > 0) {
+            const int32_t y = (int32_t)w[1];
+            const uint32_t lsh0 = 2u * (uint32_t)kCeilK0, rows0 = (wm + 1u) >> lsh0;
+            const int32_t c0 = P.ceil[P.ceil_off[0] + (int64_t)(w[2] >> lsh0) * rows0 + (w[0] >> lsh0)];
+            int32_t c1 = 32767;
+            if (P.ceil_levels > 1) {  // (uniform)
+                const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
+                c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
+            }
+            const bool p1 = y > c1;
+            cl = p1 || y > c0;
+            const uint32_t bmk = p1 ? (1u << (lsh0 + 2u)) - 1u : (1u << lsh0) - 1u;  // block width - 1
+            const int32_t c = p1 ? c1 : c0;
+            // steps to leave the box, less one: the block's faces in x / z, the ceiling (down) or the top
+            // of the world (up) in y
+            cex[0] = (int32_t)(R.s[0] > 0 ? bmk - (w[0] & bmk) : (w[0] & bmk));
+            cex[1] = R.s[1] < 0 ? y - c - 1 : (int32_t)(wm - w[1]);
+            cex[2] = (int32_t)(R.s[2] > 0 ? bmk - (w[2] & bmk) : (w[2] & bmk));
+        }
+        uint32_t kind = R_CEIL;
+        if (!cl) {
+            kind = lookup<STATS, !REFLECT, KEEPPAR>(P, mem, path, w, moved, par, sh, bmask, bref, binfo, st);
+            jump = 0u;
+        }
         if (kind == R_SOLID) {
             mat = binfo >> 16;
             done = true;
@@ -883,7 +922,18 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
                        box_exits(w, R.s, sh, par.mask, ud, ex);
-                       return skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
+                       if (ceil_on) {
+#pragma unroll
+                           for (int k = 0; k < 3; k++) ex[k] = cl ? cex[k] : ex[k];
+                       }
+                       const bool moved_ok = skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
+                       if (ceil_on && cl && moved_ok) {
+                           uint32_t wn[3];
+                           wrap3(R, wm, wn);
+                           jump |= (w[0] ^ wn[0]) | (w[1] ^ wn[1]) | (w[2] ^ wn[2]);
+                           if (STATS) st.ceil_moves++;
+                       }
+                       return moved_ok;
                    }())) {
             if (STATS && fast) st.skip_out++;
             if (fast) {
@@ -1066,6 +1116,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 20, (unsigned long long)st.wv_descents);
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
         if (st.no_progress) atomicAdd(P.stats + 16, (unsigned long long)st.no_progress);
+        atomicAdd(P.stats + 23, (unsigned long long)st.ceil_moves);
         if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
     }
     if (!TRACK && R.axis < 3u) {
@@ -1288,7 +1339,8 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<false, true, true, SEG>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
+        const Hit h = trace<false, true, true, SEG, 0, false, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr,
+                                                                    P.pos ? -1 : P.top_scene, P.top_scene);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -1329,7 +1381,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS, false, false, SEG, DIRS, AO>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS, false, false, SEG, DIRS, AO, true>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
         if (!SHADE && P.wire) {  // (wave-uniform: one launch writes one kind of record)
             wire_put(P.wire, P.wire_compact != 0, out, o, h.x, h.y, h.z, h.t, h.info);
@@ -1580,6 +1632,12 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.top_solid = t->dev_top_y;  // the empty region above the tree's highest voxel row (trace: pre_top)
+    if (!(d->flags & SVO_CAST_NO_CEILINGS)) {
+        P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
+        P.ceil_levels = std::min(t->ceil_levels, 2);
+        P.ceil_off[0] = t->ceil_off[0];
+        P.ceil_off[1] = t->ceil_off[1];
+    }
     P.steps = d->steps;
     P.flags = d->flags;
     P.stats = reinterpret_cast<unsigned long long*>(d->stats);
@@ -1648,6 +1706,9 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_pal) (void)hipFree(t->d_pal);
     if (t->d_pick) (void)hipFree(t->d_pick);
     if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
+    if (t->d_ceil) (void)hipFree(t->d_ceil);
+    t->d_ceil = nullptr;
+    t->ceil_levels = 0;
     t->d_ao_plan = nullptr;
     t->ao_plan_steps = -1;
     (void)hipSetDevice(prev);
@@ -1661,6 +1722,22 @@ extern "C" void svo_tree_destroy(svo_tree* t) {
     if (!t) return;
     tree_release_device(t);
     delete t;
+}
+
+// the column ceilings of the host image (tree_ceilings), replacing the device copy
+static int upload_ceilings(svo_tree* t) {
+    std::vector<int16_t> c;
+    int64_t off[kCeilMax] = {0, 0, 0, 0};
+    const int32_t n = tree_ceilings(t, c, off);
+    if (t->d_ceil) (void)hipFree(t->d_ceil);
+    t->d_ceil = nullptr;
+    t->ceil_levels = 0;
+    if (n == 0) return SVO_OK;
+    HIP_TRY(hipMalloc(&t->d_ceil, c.size() * sizeof(int16_t)), SVO_ENOMEM);
+    HIP_TRY(hipMemcpy(t->d_ceil, c.data(), c.size() * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    t->ceil_levels = n;
+    for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = off[j];
+    return SVO_OK;
 }
 
 static int upload_palette(svo_tree* t) {
@@ -1710,7 +1787,7 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     t->synced_mats = t->mats.size();
     t->dirty_nodes.clear();
     t->full_upload = false;
-    return SVO_OK;
+    return upload_ceilings(t);
 }
 
 int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_cap, void* d_mats, uint64_t mat_cap) {
@@ -1732,7 +1809,7 @@ int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_
     t->synced_mats = t->mats.size();
     t->dirty_nodes.clear();
     t->full_upload = false;
-    return SVO_OK;
+    return upload_ceilings(t);
 }
 
 // updateSsboData after edits (voxel_allocator.hpp:38-78): only the appended tail and the records
@@ -1765,7 +1842,7 @@ extern "C" int svo_tree_sync(svo_tree* t) {
     t->synced_nodes = t->nodes.size();
     t->dev_top_y = tree_top_y(t);
     t->synced_mats = t->mats.size();
-    return SVO_OK;
+    return upload_ceilings(t);
 }
 
 // ================================================================================================

@@ -70,10 +70,22 @@ struct svo_tree {
     mutable bool top_valid = false;
     mutable std::mutex top_mu;  // (casts from several threads compute it once)
     int32_t dev_top_y = -1;     // tree_top_y of the image in HBM (set by upload / adopt / sync; -1: none)
+    // column ceilings of the image in HBM (tree_ceilings, uploaded with it): d_ceil holds, for each
+    // level j < ceil_levels, the highest stored voxel row (int16, -1: none) of every aligned block of
+    // 4^(kCeilK0 + j) x 4^(kCeilK0 + j) columns, row-major [z][x], starting at element ceil_off[j]
+    void* d_ceil = nullptr;
+    int32_t ceil_levels = 0;
+    int64_t ceil_off[4] = {0, 0, 0, 0};
 };
 
 namespace svo {
 int32_t tree_top_y(const svo_tree* t);  // svo_world.cpp
+// Column ceilings (svo_world.cpp): per aligned block of 4^k x 4^k columns, k = kCeilK0 .. levels - 1 (at
+// most kCeilMax levels), the highest stored voxel row in those columns (-1: none) — every voxel above it
+// in the block is empty, whatever the tree holds (overhangs included).  Level j's blocks are row-major
+// [z][x] at out[off[j] ..]; returns the number of levels.
+constexpr int32_t kCeilK0 = 3, kCeilMax = 4;
+int32_t tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t off[kCeilMax]);
 void tree_release_device(svo_tree* t);  // svo_cast.hip
 // take over device arrays built on `device` (node_cap / mat_cap elements allocated, the host image
 // already equal to their first nodes.size() / mats.size() elements): svo_cast.hip

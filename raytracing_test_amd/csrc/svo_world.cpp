@@ -1015,6 +1015,90 @@ int32_t svo::tree_top_y(const svo_tree* t) {
     return t->top_y;
 }
 
+// Column ceilings: one walk over the tree fills the finest level (blocks of 4^kCeilK0 columns) with
+// the highest stored row over each block, then coarser levels take maxima of 4 x 4 blocks.
+namespace {
+struct CeilWalk {
+    const svo_tree* t;
+    int32_t bsh;   // log2 of the finest block's width
+    int64_t rows;  // finest blocks per row
+    int16_t* top;
+    void put(int64_t bx, int64_t bz, int32_t y) {
+        int16_t& c = top[bz * rows + bx];
+        if (y > c) c = (int16_t)y;
+    }
+    // region of node ni: [x0, x0 + size) x [y0, ..) x [z0, ..)
+    void walk(uint32_t ni, int32_t x0, int32_t y0, int32_t z0, int depth) {
+        const Node& n = t->nodes[ni];
+        const int32_t size = 1 << (2 * (t->levels - depth));
+        const uint32_t kind = node_kind(n.info);
+        if (kind == K_SOLID) {
+            const int64_t nb = std::max<int64_t>(1, (int64_t)size >> bsh);
+            for (int64_t bz = 0; bz < nb; bz++)
+                for (int64_t bx = 0; bx < nb; bx++) put(((int64_t)x0 >> bsh) + bx, ((int64_t)z0 >> bsh) + bz, y0 + size - 1);
+            return;
+        }
+        if (kind == K_BRICK) {
+            for (int ly = 3; ly >= 0; ly--)
+                if (n.mask & (0x000F000F000F000Full << (4 * ly))) {
+                    put((int64_t)x0 >> bsh, (int64_t)z0 >> bsh, y0 + ly);
+                    break;
+                }
+            return;
+        }
+        const int32_t cs = size >> 2;
+        uint64_t m = n.mask;
+        uint32_t ci = n.ref;
+        while (m) {
+            const uint32_t sl = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            walk(ci++, x0 + (int32_t)(sl & 3u) * cs, y0 + (int32_t)((sl >> 2) & 3u) * cs, z0 + (int32_t)(sl >> 4) * cs, depth + 1);
+        }
+    }
+};
+}  // namespace
+
+int32_t svo::tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t off[kCeilMax]) {
+    out.clear();
+    const int32_t nlev = std::min<int32_t>(kCeilMax, t->levels - kCeilK0);
+    if (nlev <= 0 || t->nodes.empty()) return 0;
+    int64_t total = 0;
+    for (int32_t j = 0; j < nlev; j++) {
+        const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
+        off[j] = total;
+        total += rows * rows;
+    }
+    out.assign((size_t)total, (int16_t)-1);
+    CeilWalk cw{t, 2 * kCeilK0, (int64_t)1 << (2 * (t->levels - kCeilK0)), out.data()};
+    cw.walk(0, 0, 0, 0, 0);
+    for (int32_t j = 1; j < nlev; j++) {  // 4 x 4 maxima of the finer level
+        const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j)), fine = rows * 4;
+        const int16_t* f = out.data() + off[j - 1];
+        int16_t* c = out.data() + off[j];
+        for (int64_t bz = 0; bz < rows; bz++)
+            for (int64_t bx = 0; bx < rows; bx++) {
+                int16_t v = -1;
+                for (int64_t dz = 0; dz < 4; dz++)
+                    for (int64_t dx = 0; dx < 4; dx++) v = std::max(v, f[(bz * 4 + dz) * fine + bx * 4 + dx]);
+                c[bz * rows + bx] = v;
+            }
+    }
+    return nlev;
+}
+
+extern "C" int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n) {
+    if (!t || !levels || !n) SVO_FAIL(SVO_EINVAL, "svo_tree_ceilings: NULL argument");
+    std::vector<int16_t> c;
+    int64_t off[kCeilMax] = {0, 0, 0, 0};
+    *levels = tree_ceilings(t, c, off);
+    *n = (int64_t)c.size();
+    if (out) {
+        if (cap < *n) SVO_FAIL(SVO_ERANGE, "svo_tree_ceilings: buffer too small");
+        if (!c.empty()) memcpy(out, c.data(), c.size() * sizeof(int16_t));
+    }
+    return SVO_OK;
+}
+
 extern "C" int svo_tree_node_indices(const svo_tree* t, const int32_t* xyz, int64_t n, uint64_t* idx) {
     if (!t || ((!xyz || !idx) && n > 0)) SVO_FAIL(SVO_EINVAL, "svo_tree_node_indices: NULL argument");
     const uint32_t mk = (1u << (2 * t->levels)) - 1u;

@@ -68,7 +68,7 @@ def test_reference_world_frames(rt, oracle_mod, gtree, ref_world_oracle, cam, st
     W = H = 256
     ref = ref_world_oracle.cast_frame(org, dn, W, H, steps)
     assert ref["rc"] == 0
-    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_WIDE_ADDR, rt.CAST_SEGMENTS, rt.CAST_NO_OCTANT, rt.CAST_SEGMENTS | rt.CAST_ITERATIVE):
+    for flags in (0, rt.CAST_ITERATIVE, rt.CAST_BOTTOM_FIRST, rt.CAST_TILE_8X8, rt.CAST_TILE_32X2, rt.CAST_WIDE_ADDR, rt.CAST_NO_CEILINGS, rt.CAST_SEGMENTS, rt.CAST_NO_OCTANT, rt.CAST_SEGMENTS | rt.CAST_ITERATIVE):
         out = gtree.cast_frame(org, dn, W, H, steps, flags=flags)
         compare(rt, gtree, out, ref, "cam%d S=%d flags=%d" % (cam, steps, flags))
 
@@ -439,7 +439,7 @@ def test_depth12_half_integral_camera(rt, depth12, oracle12, org):
     assert ref["rc"] == 0
     compare(rt, depth12, out, ref, "half-integral %s" % (org,))
     a = rt.decode_hits(out)
-    for flags in (rt.CAST_SEGMENTS, rt.CAST_ITERATIVE, rt.CAST_NO_OCTANT):
+    for flags in (rt.CAST_SEGMENTS, rt.CAST_ITERATIVE, rt.CAST_NO_OCTANT, rt.CAST_NO_CEILINGS):
         b = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384, flags=flags))
         for k in a:
             assert np.array_equal(a[k], b[k]), (org, flags, k)
@@ -484,7 +484,7 @@ def test_depth12_fractional_camera(rt, depth12, oracle12, org):
     assert np.array_equal(sub["pos"], ref["pos"]) and np.array_equal(sub["steps"], ref["steps"])
     assert np.array_equal(sub["hit"], ref["hit"] != 0) and np.array_equal(sub["last_pos"], ref["last"])
     assert np.array_equal(sub["t"], ref["t"].astype(np.float32))
-    for flags in (rt.CAST_ITERATIVE, rt.CAST_NO_OCTANT):
+    for flags in (rt.CAST_ITERATIVE, rt.CAST_NO_OCTANT, rt.CAST_NO_CEILINGS):
         o2 = rt.decode_hits(depth12.cast_frame(org, dn, W, H, 16384, flags=flags))
         for k in out:
             assert np.array_equal(out[k], o2[k]), (k, flags)
@@ -501,7 +501,9 @@ def test_depth12_full_frame_properties(rt, depth12):
     c = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_ITERATIVE))
     e = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_WIDE_ADDR))
     f = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_NO_OCTANT))
+    nc = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, flags=rt.CAST_NO_CEILINGS))
     for k in a:
+        assert np.array_equal(a[k], nc[k]), k
         assert np.array_equal(a[k], b[k]), k
         assert np.array_equal(a[k], c[k]), k
         assert np.array_equal(a[k], e[k]), k

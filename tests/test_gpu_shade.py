@@ -210,6 +210,12 @@ def test_shade_liquid_depth12_sampled(rt, oracle_mod, torch_cuda):
     ref = ot.shade_frame(org, cam_dir, W, H, 16384, rt.sun_dir(), pixels=pix, liquid=True, time=1.25)
     g = rt.decode_hits(hits)
     _check(rgba[torch_cuda.as_tensor(pix, device=rgba.device)], ref, g["hit"][pix], "depth12 lakes")
+    # column-ceiling moves (primary and refracted rays) change nothing: the whole image and its records
+    rgba2, hits2 = tree.shade_frame(org, cam_dir, W, H, 16384, sun=rt.sun_dir(), with_hits=True, scene=scene, time=1.25,
+                                    flags=rt.CAST_NO_CEILINGS)
+    assert torch_cuda.equal(rgba, rgba2)
+    for k in hits:
+        assert torch_cuda.equal(hits[k], hits2[k]), k
 
 
 def test_full_view_tree_is_not_castable(rt, lake_scene):

@@ -310,3 +310,40 @@ def test_tree_checkpoint_rejects_damage(rt, ref_tree, tmp_path):
                             ("cycle.svo", point_back, "reached twice")):
         with pytest.raises(RuntimeError, match=msg):
             rt.Tree.load(resealed(edit, name))
+
+
+@pytest.mark.parametrize("view", [0, 1])
+def test_column_ceilings(rt, view):
+    """svo_tree_ceilings (what the casts' ceiling moves rely on): per aligned block of 4^k x 4^k columns the highest
+    stored row — for a terrain tree, the column tops (water up to row 20 above tops below it in the full view)
+    maximised over the block; -1 over columns that hold nothing"""
+    W, L = 300, 700
+    t = rt.Tree.terrain(5, W, L, view=view)
+    H = rt.terrain_heights(W, L).astype(np.int64)
+    top = np.full((1024, 1024), -1, np.int64)  # [x, z]
+    top[:W, :L] = np.where(H < 20, 20, H) if view == rt.VIEW_ALL else H
+    cs = t.ceilings()
+    assert len(cs) == 2  # k = 3, 4 (64- and 256-column blocks) below the 1024-wide world
+    for j, c in enumerate(cs):
+        B = 4 ** (3 + j)
+        want = top.reshape(1024 // B, B, 1024 // B, B).max(axis=(1, 3))
+        assert np.array_equal(c.astype(np.int64), want.T), j
+
+
+def test_column_ceilings_edited_world(rt, ref_world):
+    """the reference world (putBlock / genWorld + the debug blocks: (10,100,10) and (1000,1000,1000)) and an edit:
+    each probed block's ceiling equals the highest stored row getBlock finds in its columns"""
+    w = rt.World.reference()
+    w.put_block(700, 611, 300, 0, 12345, 0.0)  # a floating voxel
+    t = w.build(rt.VIEW_ALL)
+    c64 = t.ceilings()[0]
+    for bx, bz in ((0, 0), (15, 15), (10, 4), (3, 3)):
+        xs, zs, ys = np.arange(bx * 64, bx * 64 + 64), np.arange(bz * 64, bz * 64 + 64), np.arange(1024)
+        best = -1
+        for y0 in range(0, 1024, 128):  # (in slabs: 64 x 64 x 128 lookups at a time)
+            g = np.stack(np.meshgrid(xs, ys[y0:y0 + 128], zs, indexing="ij"), -1).reshape(-1, 3)
+            _, col, _ = w.get_blocks(g)
+            stored = col != np.uint64(0xFFFFFFFFFFFFFFFF)
+            if stored.any():
+                best = max(best, int(g[stored][:, 1].max()))
+        assert c64[bz, bx] == best, (bx, bz, c64[bz, bx], best)
