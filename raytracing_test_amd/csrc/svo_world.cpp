@@ -1070,7 +1070,26 @@ int32_t svo::tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t
     }
     out.assign((size_t)total, (int16_t)-1);
     CeilWalk cw{t, 2 * kCeilK0, (int64_t)1 << (2 * (t->levels - kCeilK0)), out.data()};
-    cw.walk(0, 0, 0, 0, 0);
+    const Node& root = t->nodes[0];
+    if (node_kind(root.info) != K_INTERIOR) {
+        cw.walk(0, 0, 0, 0, 0);
+    } else {
+        // the root's children by column (x, z slot): each thread walks the four children over one
+        // quarter x quarter of the columns, so the blocks it writes are its own
+        const int32_t cs = 1 << (2 * (t->levels - 1));
+        std::vector<std::thread> th;
+        for (uint32_t xz = 0; xz < 16; xz++)
+            th.emplace_back([&, xz] {
+                CeilWalk w = cw;
+                for (uint32_t y = 0; y < 4; y++) {
+                    const uint32_t sl = ((xz >> 2) << 4) | (y << 2) | (xz & 3u);
+                    if (!((root.mask >> sl) & 1ull)) continue;
+                    const uint32_t ci = root.ref + (uint32_t)__builtin_popcountll(root.mask & ((1ull << sl) - 1ull));
+                    w.walk(ci, (int32_t)(xz & 3u) * cs, (int32_t)y * cs, (int32_t)(xz >> 2) * cs, 1);
+                }
+            });
+        for (auto& x : th) x.join();
+    }
     for (int32_t j = 1; j < nlev; j++) {  // 4 x 4 maxima of the finer level
         const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j)), fine = rows * 4;
         const int16_t* f = out.data() + off[j - 1];
