@@ -861,7 +861,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     uint32_t bref = 0u, binfo = 0u;
     uint64_t bmask = 0ull;
     bool escaped = false;
-    // coordinate bits changed by ceiling moves since the last lookup (the lookup's restart depth)
+    // coordinate bits changed since the last voxel known to lie in the parent's region, by ceiling moves since
+    // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
     const bool ceil_on = CEIL && P.ceil_levels > 0;  // (uniform)
     while (!done) {
@@ -928,9 +929,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        }
                        const bool moved_ok = skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                        if (ceil_on && cl && moved_ok) {
+                           // (the voxel this move started from need not lie in the parent's region: the step
+                           // that entered it — `moved` — counts too)
                            uint32_t wn[3];
                            wrap3(R, wm, wn);
-                           jump |= (w[0] ^ wn[0]) | (w[1] ^ wn[1]) | (w[2] ^ wn[2]);
+                           jump = moved | (w[0] ^ wn[0]) | (w[1] ^ wn[1]) | (w[2] ^ wn[2]);
                            if (STATS) st.ceil_moves++;
                        }
                        return moved_ok;
