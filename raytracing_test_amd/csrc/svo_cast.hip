@@ -95,6 +95,12 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+#ifndef SVO_CEIL_LEVELS
+#define SVO_CEIL_LEVELS 2  // column-ceiling levels the traversal checks: 64-column blocks, then 256 (A/B: 1)
+#endif
+#ifndef SVO_CEIL_CACHE
+#define SVO_CEIL_CACHE 0   // A/B: keep the lane's block ceilings in registers until it changes block
+#endif
 #ifndef SVO_SHADE_WAVES
 #define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
 #endif
@@ -865,6 +871,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
     const bool ceil_on = CEIL && P.ceil_levels > 0;  // (uniform)
+#if SVO_CEIL_CACHE
+    uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 64-column block (key) and its ceilings (c0 | c1 << 16)
+#endif
     while (!done) {
         // the voxel just entered is untested
         if (STATS) st.wv_iters += wave_lead();
@@ -890,12 +899,27 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = 2u * (uint32_t)kCeilK0, rows0 = (wm + 1u) >> lsh0;
-            const int32_t c0 = P.ceil[P.ceil_off[0] + (int64_t)(w[2] >> lsh0) * rows0 + (w[0] >> lsh0)];
+            const uint32_t key = (w[2] >> lsh0) * rows0 + (w[0] >> lsh0);
+#if SVO_CEIL_CACHE
+            // (the lane's block and its ceilings stay in registers until it moves to another 64-column block)
+            if (key != ckey) {
+                ckey = key;
+                int32_t c1 = 32767;
+                if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
+                    const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
+                    c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
+                }
+                cval = ((uint32_t)(uint16_t)P.ceil[P.ceil_off[0] + (int64_t)key]) | ((uint32_t)c1 << 16);
+            }
+            const int32_t c0 = (int32_t)(int16_t)(cval & 0xFFFFu), c1 = (int32_t)cval >> 16;
+#else
+            const int32_t c0 = P.ceil[P.ceil_off[0] + (int64_t)key];
             int32_t c1 = 32767;
-            if (P.ceil_levels > 1) {  // (uniform)
+            if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
                 const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
                 c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
             }
+#endif
             const bool p1 = y > c1;
             cl = p1 || y > c0;
             const uint32_t bmk = p1 ? (1u << (lsh0 + 2u)) - 1u : (1u << lsh0) - 1u;  // block width - 1
