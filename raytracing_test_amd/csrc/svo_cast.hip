@@ -99,7 +99,7 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #define SVO_CEIL_LEVELS 2  // column-ceiling levels the traversal checks: 64-column blocks, then 256 (A/B: 1)
 #endif
 #ifndef SVO_CEIL_CACHE
-#define SVO_CEIL_CACHE 0   // A/B: keep the lane's block ceilings in registers until it changes block
+#define SVO_CEIL_CACHE 1   // keep the lane's block ceilings in registers until it changes block (A/B: 0 loads them every iteration)
 #endif
 #ifndef SVO_SHADE_WAVES
 #define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
@@ -895,7 +895,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         // whole block: that box is crossed without a lookup (R_CEIL; the next lookup restarts from the
         // per-lane path at the depth the moves since the last lookup left intact)
         int32_t cex[3] = {0, 0, 0};
-        bool cl = false;
+        bool cl = false, any_cl = false;
+        int32_t c0 = -1, c1 = 32767;  // the ceilings of the lane's 64- and 256-column blocks
         if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = 2u * (uint32_t)kCeilK0, rows0 = (wm + 1u) >> lsh0;
@@ -911,10 +912,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 }
                 cval = ((uint32_t)(uint16_t)P.ceil[P.ceil_off[0] + (int64_t)key]) | ((uint32_t)c1 << 16);
             }
-            const int32_t c0 = (int32_t)(int16_t)(cval & 0xFFFFu), c1 = (int32_t)cval >> 16;
+            c0 = (int32_t)(int16_t)(cval & 0xFFFFu);
+            c1 = (int32_t)cval >> 16;
 #else
-            const int32_t c0 = P.ceil[P.ceil_off[0] + (int64_t)key];
-            int32_t c1 = 32767;
+            c0 = P.ceil[P.ceil_off[0] + (int64_t)key];
             if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
                 const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
                 c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
@@ -922,6 +923,12 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
 #endif
             const bool p1 = y > c1;
             cl = p1 || y > c0;
+        }
+        any_cl = ceil_on && __ballot(cl) != 0ull;  // (wave-uniform: the box exits only when a lane moves)
+        if (any_cl) {
+            const int32_t y = (int32_t)w[1];
+            const uint32_t lsh0 = 2u * (uint32_t)kCeilK0;
+            const bool p1 = y > c1;
             const uint32_t bmk = p1 ? (1u << (lsh0 + 2u)) - 1u : (1u << lsh0) - 1u;  // block width - 1
             const int32_t c = p1 ? c1 : c0;
             // steps to leave the box, less one: the block's faces in x / z, the ceiling (down) or the top
@@ -947,7 +954,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
                        box_exits(w, R.s, sh, par.mask, ud, ex);
-                       if (ceil_on) {
+                       if (any_cl) {
 #pragma unroll
                            for (int k = 0; k < 3; k++) ex[k] = cl ? cex[k] : ex[k];
                        }
