@@ -4,7 +4,7 @@
 Workload (the default): genWorld's terrain on 4096 x 4096 columns as a
 depth-12 (4096^3, 6-level) tree, one 1920x1080 frame of primary rays from (4,90,4) towards
 normalize(1,-0.45,1), step budget 16384, castRayFromCam semantics (every ray ends on terrain).
-Other configs: --config c1 (dense 256^3 grid, 256^2 rays), c2 / c2cam0 (the reference world),
+Other configs: --config c1 (dense 256^3 grid, 256^2 rays), c2 / c2cam0 (the reference world), c2d8 (genWorld in a depth-8 tree),
 c5 (depth-14, 4K); --ao N (C4: + N hemisphere AO rays per hit); --shade (the shading pass).
 
 A "step" = one pass of the cast kernel over the step's frames.  Multi-GPU (one process per GPU,
@@ -60,6 +60,9 @@ CONFIGS = {
                    label="C2: the reference world (5 levels, 1024^3), 1920x1080, the reference's default camera (globals.cpp:20-21)",
                    bray="C2_cam0_S300",
                    metric="primary rays/sec at 1080p, reference-world SVO (config 2); achieved HBM GB/s vs roofline"),
+    "c2d8": dict(levels=4, cols=200, W=1920, H=1080, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=300, shift=8.0,
+                 label="C2 as BASELINE.json words it: depth-8 SVO (4 levels, 256^3), genWorld putBlocks over 200x200 columns, 1920x1080",
+                 bray="C2d8", metric="primary rays/sec at 1080p, depth-8 SVO (config 2); achieved HBM GB/s vs roofline"),
     "c3": dict(levels=6, cols=4096, W=1920, H=1080, origin=(4.0, 90.0, 4.0), cam=(1.0, -0.45, 1.0), steps=16384, shift=64.0,
                label="C3: depth-12 SVO (4096^2 terrain columns, 6 levels, 4096^3), 1920x1080", bray="C3",
                metric="primary rays/sec at 1080p, depth-12 SVO; achieved HBM GB/s vs roofline"),
@@ -140,7 +143,9 @@ def cpu_baseline(args, cfg, ppx, ppy, gpu):
     dn = O.normalize(cfg["cam"])
     org = cfg["origin"]
     t0 = time.perf_counter()
-    if args.config.startswith("c2") or args.config == "c1":
+    if args.config == "c2d8":
+        T = O.Tree.terrain_putblock(4, 200, 200, native=True)
+    elif args.config.startswith("c2") or args.config == "c1":
         T = O.Tree.reference_world(native=True)
     elif args.config == "c5":
         # every C5 ray lands within ~2,600 voxels of the camera: the oracle's tree over the first 4096^2
@@ -380,6 +385,13 @@ def main():
         builder = "host (putBlock)"
         build_s = time.time() - t0
         tree.upload(dev)
+    elif args.config == "c2d8":  # a clean depth-8 root + genWorld, putBlock by putBlock
+        w8 = rt.World(4)
+        w8.gen_world(200, 200)
+        tree = w8.build()
+        builder = "host (putBlock)"
+        build_s = time.time() - t0
+        tree.upload(dev)
     elif args.config.startswith("c2"):  # initTetraHexaTree + genWorld, putBlock by putBlock
         tree = rt.World.reference().build()
         builder = "host (putBlock)"
@@ -395,8 +407,8 @@ def main():
         build_s = time.time() - t0
     scene = None
     if args.shade:  # the shading scene: every block, water included (it refracts, low_res.frag:214-229)
-        if args.config in ("c1", "c2", "c2cam0"):
-            scene = (rt.World.reference() if args.config != "c1" else w4).build(rt.VIEW_ALL).upload(dev)
+        if args.config in ("c1", "c2", "c2cam0", "c2d8"):
+            scene = {"c1": lambda: w4, "c2d8": lambda: w8}.get(args.config, rt.World.reference)().build(rt.VIEW_ALL).upload(dev)
         elif args.host_build:
             scene = rt.Tree.terrain(cfg["levels"], cfg["cols"], cfg["cols"], nthreads=16, view=rt.VIEW_ALL).upload(dev)
         else:
@@ -620,6 +632,7 @@ def main():
         "dtype": "f64",
         "data": ("synthetic: the reference world (initTetraHexaTree + genWorld on 200x200 columns), built in-process"
                  if args.config in ("c1", "c2", "c2cam0") else
+                 "synthetic: a clean depth-8 root + genWorld on 200x200 columns, built in-process" if args.config == "c2d8" else
                  "synthetic: genWorld OpenSimplex terrain (seeds 42/64/100) on %dx%d columns, built in-process" % (cfg["cols"], cfg["cols"])),
         "config": {"workload": work + cfg["label"] + " primary rays per frame, camera (%g,%g,%g)->normalize(%g,%g,%g), S=%d, "
                                                      "castRayFromCam semantics" % (cfg["origin"] + cfg["cam"] + (STEPS,)),

@@ -28,7 +28,22 @@ def c3f_entry():
             "tree": "as C3, camera at %s (non-integral: segment-exact crossings)" % (C3F_ORIGIN,)}
 
 
+def c2d8_entry():
+    # BASELINE.json config 2 as worded: depth 8 = a 4-level (256^3) tree, putBlock / genWorld over 200 x 200 columns
+    t = O.Tree.terrain_putblock(4, 200, 200)
+    e = t.frame_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 300, nthreads=8) / (1920 * 1080)
+    return {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
+            "tree": "depth-8 (4 levels, 256^3): clean root + genWorld putBlocks over 200 x 200 columns; C3 pose, S = 300"}
+
+
 def main():
+    if sys.argv[1:] == ["C2d8"]:
+        path = os.path.join(ROOT, "profiles", "bray.json")
+        res = json.load(open(path))
+        res["C2d8"] = c2d8_entry()
+        json.dump(res, open(path, "w"), indent=1)
+        print(json.dumps(res["C2d8"], indent=1))
+        return
     if sys.argv[1:] == ["C3f"]:
         path = os.path.join(ROOT, "profiles", "bray.json")
         res = json.load(open(path))
@@ -48,6 +63,7 @@ def main():
     res["C3"] = {"e_child_per_ray": e, "bytes_per_ray": 16 * (e + 1) + 4 * e + B_OUT,
                  "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
     res["C3f"] = c3f_entry()
+    res["C2d8"] = c2d8_entry()
     # C4: §8(d) "for AO: add <= 5 steps x E per sample" -- the AO rays' node entries (each continues the
     # restart model from the primary's final lookup), 16 + 4 B per entry, per primary ray of the frame;
     # B_OUT grows by the 1-B AO count

@@ -10,3 +10,4 @@ L="variants/libsvo_base.so variants/libsvo_c2.so default"
 run ab_c3 900 env REPS=4 bash tools/ab_lib.sh r03_f_c3 $L
 run ab_c5 900 env REPS=2 BENCH_ARGS="--config c5" bash tools/ab_lib.sh r03_f_c5 $L
 run ab_shade 900 env REPS=2 BENCH_ARGS="--shade --pipelined-steps 0" bash tools/ab_lib.sh r03_f_sh $L
+run c2d8 300 python -u bench.py --config c2d8 --steps 50 --warmup 10
