@@ -101,6 +101,9 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #ifndef SVO_CEIL_CACHE
 #define SVO_CEIL_CACHE 1   // keep the lane's block ceilings in registers until it changes block (A/B: 0 loads them every iteration)
 #endif
+#ifndef SVO_CEIL_GATE
+#define SVO_CEIL_GATE 0    // A/B: 1 gates the ceiling box exits by a ballot in the primary instances too
+#endif
 #ifndef SVO_SHADE_WAVES
 #define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
 #endif
@@ -924,7 +927,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             const bool p1 = y > c1;
             cl = p1 || y > c0;
         }
-        any_cl = ceil_on && __ballot(cl) != 0ull;  // (wave-uniform: the box exits only when a lane moves)
+        // (the shading instances take the box exits only when a lane of the wave moves — wave-uniform; the
+        // primary ones select them per lane; the two measured equal within 1 %: profiles/r03/ab_f_*.log, ab_g_*.log)
+        any_cl = ceil_on && ((!REFLECT && !SVO_CEIL_GATE) || __ballot(cl) != 0ull);
         if (any_cl) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = 2u * (uint32_t)kCeilK0;

@@ -17,6 +17,7 @@ b c4_ao20 --ao 20 --no-cpu-baseline
 b c5 --config c5
 b c2 --config c2
 b c2cam0 --config c2cam0 --no-cpu-baseline
+b c2d8 --config c2d8
 b shade --shade
 b xchg1 --force-exchange --verify --no-cpu-baseline
 b xchg1_ao --force-exchange --verify --no-cpu-baseline --ao 16
