@@ -554,15 +554,18 @@ class Tree:
         return out
 
     def ceilings(self):
-        """the column ceilings (svo_tree_ceilings): a list of (E / 4^k) x (E / 4^k) int16 arrays [z][x], k = 3, 4, ..."""
+        """the column ceilings (svo_tree_ceilings): a list of (E / 4^k) x (E / 4^k) int16 arrays [z][x], k = k0, k0 + 1, ... (k0 = 3 unless built otherwise)"""
         lv, n = C.c_int32(), C.c_int64()
         _check(lib().svo_tree_ceilings(self._h, None, 0, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
         out = np.zeros(n.value, np.int16)
         _check(lib().svo_tree_ceilings(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
         E = 1 << (2 * self.info().levels)
+        # the finest level's blocks are 4^k0 columns wide (SVO_CEIL_K0, 3 by default): the one k0 whose level sizes add up to n
+        k0 = next(k for k in range(1, 8) if sum((E >> (2 * (k + j))) ** 2 for j in range(lv.value)) == n.value) if lv.value else 3
+        self.ceil_k0 = k0
         res, off = [], 0
         for j in range(lv.value):
-            rows = E >> (2 * (3 + j))
+            rows = E >> (2 * (k0 + j))
             res.append(out[off:off + rows * rows].reshape(rows, rows))
             off += rows * rows
         return res

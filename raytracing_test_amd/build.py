@@ -43,8 +43,8 @@ def build(force=False, verbose=False, out=None, build_dir=None, defines=(), flag
         src = os.path.join(CSRC, s)
         obj = os.path.join(BUILD_, s + ".o")
         if force or _newer(obj, [src] + hdrs):
-            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-Wall",
-                  "-c", src, "-o", obj])
+            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-Wall"] +
+                 ["-D" + d for d in defines] + ["-c", src, "-o", obj])
         objs.append(obj)
     for s in HIP_SRCS:
         src = os.path.join(CSRC, s)

@@ -87,10 +87,12 @@ struct CastParams {
     // the highest stored voxel row of the scene / of the solid tree (tree_top_y; casts: top_solid); a ray
     // moving up above it that cannot wrap in y before its budget ends can hit nothing more
     int32_t top_scene, top_solid;
-    // column ceilings of the tree the rays walk (the scene, for shading): level j's blocks are 4^(kCeilK0 + j)
-    // columns wide, row-major at ceil + ceil_off[j] (svo_internal.h tree_ceilings); ceil_levels 0: none
+    // column ceilings of the tree the rays walk (the scene, for shading): two levels of the tree's table
+    // (set_ceilings), blocks 2^ceil_sh[j] columns wide, row-major at ceil + ceil_off[j] (svo_internal.h
+    // tree_ceilings); ceil_levels: how many of the two the tree has
     const int16_t* ceil;
     int32_t ceil_levels;
+    uint32_t ceil_sh[2];
     int64_t ceil_off[2];
 };
 
@@ -103,6 +105,9 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #endif
 #ifndef SVO_CEIL_GATE
 #define SVO_CEIL_GATE 0    // A/B: 1 gates the ceiling box exits by a ballot in the primary instances too
+#endif
+#ifndef SVO_PRIO_TOP
+#define SVO_PRIO_TOP 0     // A/B: tile rows from the top whose waves raise their issue priority
 #endif
 #ifndef SVO_SHADE_WAVES
 #define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
@@ -902,7 +907,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         int32_t c0 = -1, c1 = 32767;  // the ceilings of the lane's 64- and 256-column blocks
         if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
-            const uint32_t lsh0 = 2u * (uint32_t)kCeilK0, rows0 = (wm + 1u) >> lsh0;
+            const uint32_t lsh0 = P.ceil_sh[0], rows0 = (wm + 1u) >> lsh0;
+            const uint32_t lsh1 = P.ceil_sh[1], rows1 = (wm + 1u) >> lsh1;
             const uint32_t key = (w[2] >> lsh0) * rows0 + (w[0] >> lsh0);
 #if SVO_CEIL_CACHE
             // (the lane's block and its ceilings stay in registers until it moves to another 64-column block)
@@ -910,7 +916,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 ckey = key;
                 int32_t c1 = 32767;
                 if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
-                    const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
                     c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
                 }
                 cval = ((uint32_t)(uint16_t)P.ceil[P.ceil_off[0] + (int64_t)key]) | ((uint32_t)c1 << 16);
@@ -920,7 +925,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
 #else
             c0 = P.ceil[P.ceil_off[0] + (int64_t)key];
             if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
-                const uint32_t lsh1 = lsh0 + 2u, rows1 = rows0 >> 2;
                 c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
             }
 #endif
@@ -932,9 +936,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         any_cl = ceil_on && ((!REFLECT && !SVO_CEIL_GATE) || __ballot(cl) != 0ull);
         if (any_cl) {
             const int32_t y = (int32_t)w[1];
-            const uint32_t lsh0 = 2u * (uint32_t)kCeilK0;
             const bool p1 = y > c1;
-            const uint32_t bmk = p1 ? (1u << (lsh0 + 2u)) - 1u : (1u << lsh0) - 1u;  // block width - 1
+            const uint32_t bmk = (1u << (p1 ? P.ceil_sh[1] : P.ceil_sh[0])) - 1u;  // block width - 1
             const int32_t c = p1 ? c1 : c0;
             // steps to leave the box, less one: the block's faces in x / z, the ceiling (down) or the top
             // of the world (up) in y
@@ -1339,6 +1342,10 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
         if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
+#if SVO_PRIO_TOP > 0
+        // A/B: the top tile rows (the launch's longest waves, dispatched first) win issue arbitration
+        if (trl >= P.tile_rows_local - SVO_PRIO_TOP) __builtin_amdgcn_s_setprio(3);
+#endif
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
@@ -1662,6 +1669,23 @@ static void frame_axes(CastParams& P, int dirs) {
         }
 }
 
+// The two ceiling levels a launch checks, as levels of the tree's table (4^(kCeilK0 + j) columns per block).
+// Primary casts: 16 and 64 columns (C3 0.1824 -> 0.1787 ms, C5 0.562 -> 0.543 against 64 / 256; 16 / 256 was
+// slower than both: profiles/r03/ab_j_*.log).  Shading: 64 and 256 (16 / 64 measured 0.62 -> 0.80 ms there).
+constexpr int kCeilPrimary[2] = {0, 1}, kCeilShade[2] = {1, 2};
+
+static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& P, const int lv[2]) {
+    P.ceil = nullptr;
+    P.ceil_levels = 0;
+    if (d->flags & SVO_CAST_NO_CEILINGS) return;
+    P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
+    P.ceil_levels = t->ceil_levels > lv[1] ? 2 : (t->ceil_levels > lv[0] ? 1 : 0);
+    for (int j = 0; j < 2; j++) {
+        P.ceil_sh[j] = 2u * (uint32_t)(kCeilK0 + lv[j]);
+        P.ceil_off[j] = t->ceil_off[lv[j]];
+    }
+}
+
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
@@ -1671,12 +1695,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.top_solid = t->dev_top_y;  // the empty region above the tree's highest voxel row (trace: pre_top)
-    if (!(d->flags & SVO_CAST_NO_CEILINGS)) {
-        P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
-        P.ceil_levels = std::min(t->ceil_levels, 2);
-        P.ceil_off[0] = t->ceil_off[0];
-        P.ceil_off[1] = t->ceil_off[1];
-    }
+    set_ceilings(t, d, P, kCeilPrimary);
     P.steps = d->steps;
     P.flags = d->flags;
     P.stats = reinterpret_cast<unsigned long long*>(d->stats);
@@ -1909,6 +1928,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     int64_t n = 0;
     int rc = fill_params(sc, d, o ? o : &none, P, n);
     if (rc) return rc;
+    set_ceilings(sc, d, P, kCeilShade);
     P.snodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.smats = reinterpret_cast<const uint16_t*>(t->d_mats);
     P.time = sd->time;

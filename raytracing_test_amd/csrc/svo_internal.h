@@ -84,7 +84,7 @@ int32_t tree_top_y(const svo_tree* t);  // svo_world.cpp
 // most kCeilMax levels), the highest stored voxel row in those columns (-1: none) — every voxel above it
 // in the block is empty, whatever the tree holds (overhangs included).  Level j's blocks are row-major
 // [z][x] at out[off[j] ..]; returns the number of levels.
-constexpr int32_t kCeilK0 = 3, kCeilMax = 4;
+constexpr int32_t kCeilK0 = 2, kCeilMax = 4;  // 16-, 64-, 256- and 1024-column blocks
 int32_t tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t off[kCeilMax]);
 void tree_release_device(svo_tree* t);  // svo_cast.hip
 // take over device arrays built on `device` (node_cap / mat_cap elements allocated, the host image

@@ -323,9 +323,9 @@ def test_column_ceilings(rt, view):
     top = np.full((1024, 1024), -1, np.int64)  # [x, z]
     top[:W, :L] = np.where(H < 20, 20, H) if view == rt.VIEW_ALL else H
     cs = t.ceilings()
-    assert len(cs) == 2  # k = 3, 4 (64- and 256-column blocks) below the 1024-wide world
+    assert len(cs) == 5 - t.ceil_k0  # k = 3, 4 (64- and 256-column blocks) below the 1024-wide world
     for j, c in enumerate(cs):
-        B = 4 ** (3 + j)
+        B = 4 ** (t.ceil_k0 + j)
         want = top.reshape(1024 // B, B, 1024 // B, B).max(axis=(1, 3))
         assert np.array_equal(c.astype(np.int64), want.T), j
 
@@ -336,7 +336,7 @@ def test_column_ceilings_edited_world(rt, ref_world):
     w = rt.World.reference()
     w.put_block(700, 611, 300, 0, 12345, 0.0)  # a floating voxel
     t = w.build(rt.VIEW_ALL)
-    c64 = t.ceilings()[0]
+    c64 = t.ceilings()[3 - t.ceil_k0]  # (the 64-column level)
     for bx, bz in ((0, 0), (15, 15), (10, 4), (3, 3)):
         xs, zs, ys = np.arange(bx * 64, bx * 64 + 64), np.arange(bz * 64, bz * 64 + 64), np.arange(1024)
         best = -1
