@@ -109,6 +109,12 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #ifndef SVO_PRIO_TOP
 #define SVO_PRIO_TOP 0     // A/B: tile rows from the top whose waves raise their issue priority
 #endif
+#ifndef SVO_DROP_TOP
+#define SVO_DROP_TOP 0     // diagnostics only (A/B of the critical path): the top tile rows cast nothing
+#endif
+#ifndef SVO_ITER_CAP
+#define SVO_ITER_CAP 0     // diagnostics only: rays still running after this many traversal iterations stop (steps_left -1)
+#endif
 #ifndef SVO_SHADE_WAVES
 #define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
 #endif
@@ -480,6 +486,7 @@ struct Stats {
     uint32_t wv_skips, wv_descents;                // wave-level crossings, descent levels
     uint32_t no_progress;                          // loop iterations that consumed no budget (the guard's trips: 0)
     uint32_t ceil_moves;                           // crossings of a column-ceiling box (no lookup)
+    uint32_t iters;                                // this lane's traversal iterations
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -851,7 +858,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -882,9 +889,22 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
 #if SVO_CEIL_CACHE
     uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 64-column block (key) and its ceilings (c0 | c1 << 16)
 #endif
+#if SVO_ITER_CAP > 0
+    int32_t iters = 0;
+    bool capped = false;
+#endif
     while (!done) {
         // the voxel just entered is untested
-        if (STATS) st.wv_iters += wave_lead();
+        if (STATS) {
+            st.wv_iters += wave_lead();
+            st.iters++;
+        }
+#if SVO_ITER_CAP > 0
+        if (++iters > SVO_ITER_CAP) {
+            capped = true;
+            break;
+        }
+#endif
         const int32_t steps_in = R.steps;  // (the progress guard below)
         uint32_t w[3];
         wrap3(R, wm, w);
@@ -1126,6 +1146,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
     // whose budget ends in empty space take their last steps together).  Every other way out of
     // the loop without a hit has spent the budget.
+#if SVO_ITER_CAP > 0
+    if (capped) escaped = true;
+#endif
     if (!hit && !escaped) {
         while (R.steps > 0) {
             dda_step(R);
@@ -1159,7 +1182,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
         if (st.no_progress) atomicAdd(P.stats + 16, (unsigned long long)st.no_progress);
         atomicAdd(P.stats + 23, (unsigned long long)st.ceil_moves);
-        if (ray_work) *ray_work = (unsigned long long)st.lookups | ((unsigned long long)st.brick_steps << 32);
+        // per-ray work (offline analysis, bench.py SVO_RAY_WORK): 16-bit fields, lookups | iterations | brick steps | node loads
+        if (ray_work)
+            *ray_work = (unsigned long long)min(st.lookups, 65535u) | ((unsigned long long)min(st.iters, 65535u) << 16) |
+                        ((unsigned long long)min(st.brick_steps, 65535u) << 32) | ((unsigned long long)min(st.loads, 65535u) << 48);
     }
     if (!TRACK && R.axis < 3u) {
         // the last step's crossing: T - a exactly (exact sums); an infinite absDelta only comes
@@ -1173,6 +1199,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     h.y = R.r[1];
     h.z = R.r[2];
     h.steps_left = hit ? R.steps : 0;
+#if SVO_ITER_CAP > 0
+    if (capped) h.steps_left = -1;
+#endif
     h.t = (float)R.tlast;  // (one rounding of the same double as before)
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
@@ -1353,7 +1382,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
         const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
         const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+        if (trl >= 0 && trl < P.tile_rows_local - SVO_DROP_TOP && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
             o[0] = P.frame_org[3 * fr + 0];
             o[1] = P.frame_org[3 * fr + 1];
