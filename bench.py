@@ -675,15 +675,24 @@ class TorchExchange:
         self.nbuf = nbuf
         self.wire = not args.shade
         self.outs = outs
-        self.desc = None
         # frames sent per destination rank: frame f -> rank f % world; receive my frames from every rank
         self.mine = list(range(rank, self.nframes, world))
+        self.desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
+                                       frame_origins=origins if self.nframes > 1 else None)
+        self.src_descs = {f: [rt.Tree.frame_desc(origins[f], cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world)
+                              for r in range(world)] for f in self.mine}
+        # one record per row, svo_wire_bytes(desc) wide (8 B compact from integral / half-integral camera positions,
+        # else 12 B): the all-to-all splits count records, so the rows must be the packed stride.  Every frame's own
+        # shard descs must agree with the launch's format (the configs shift their frames by whole voxels)
+        self.wb = tree.wire_bytes(self.desc)
+        if any(tree.wire_bytes(d) != self.wb for ds in self.src_descs.values() for d in ds):
+            raise RuntimeError("frames of one launch with different wire formats (integral and fractional camera positions)")
         self.sends, self.recvs = [], []
         for b in range(nbuf):
             snd, rcv = [], []
             if self.wire:
-                snd.append(torch.zeros((n_mine * self.nframes, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
-                rcv.append(torch.zeros((max(1, len(self.mine)) * W * H, rt.WIRE_BYTES), dtype=torch.uint8, device=gdev))
+                snd.append(torch.zeros((n_mine * self.nframes, self.wb), dtype=torch.uint8, device=gdev))
+                rcv.append(torch.zeros((max(1, len(self.mine)) * W * H, self.wb), dtype=torch.uint8, device=gdev))
             if args.ao:
                 snd.append(outs[b]["ao"])
                 rcv.append(torch.zeros(max(1, len(self.mine)) * W * H, dtype=torch.uint8, device=gdev))
@@ -694,10 +703,6 @@ class TorchExchange:
             self.recvs.append(rcv)
         self.host = args.dist_backend != "nccl"
         self.recv_host = [[torch.empty_like(x, device="cpu") for x in r] for r in self.recvs] if self.host else None
-        self.desc = rt.Tree.frame_desc(origins[0], cam, W, H, STEPS, ppx, ppy, tile_row_start=rank, tile_row_step=world,
-                                       frame_origins=origins if self.nframes > 1 else None)
-        self.src_descs = {f: [rt.Tree.frame_desc(origins[f], cam, W, H, STEPS, ppx, ppy, tile_row_start=r, tile_row_step=world)
-                              for r in range(world)] for f in self.mine}
         self.frames = rt.Tree.alloc_hits(max(1, len(self.mine)) * W * H, gdev.index) if self.wire else None
         self.pending = {}
 

@@ -1,0 +1,44 @@
+"""bench.py's N > 1 gather on one GPU: two gloo ranks (one process each, sharing the card) cast their tile rows of
+the step's frames, exchange the wire records through torch.distributed (TorchExchange) and verify every displayed
+frame against a one-GPU cast (--verify -> gather_verified).  Weak mode sends frame f to rank f, so the all-to-all
+splits fall inside a rank's packed records: the compact 8-B format (integral camera, C3) and the 12-B one (the
+fractional C3 camera) both.  (Round 3 sized the rows at 12 B for 8-B records, and weak-mode frames did not verify.)"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(port, *extra):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--verify", "--no-cpu-baseline"] + list(extra)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert line, p.stdout[-2000:]
+    return json.loads(line[-1])
+
+
+@pytest.mark.parametrize("config,port", [("c3", 29611), ("c3f", 29612)])
+def test_weak_gather_verified(config, port):
+    d = _run(port, "--config", config)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["gather_verified"] is True, d
+
+
+def test_strong_two_frames_verified():
+    d = _run(29613, "--frames", "2")
+    assert d["scaling"] == "strong"
+    assert d["gather_verified"] is True, d
