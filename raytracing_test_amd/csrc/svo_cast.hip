@@ -103,6 +103,9 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #ifndef SVO_CEIL_CACHE
 #define SVO_CEIL_CACHE 1   // keep the lane's block ceilings in registers until it changes block (A/B: 0 loads them every iteration)
 #endif
+#ifndef SVO_CEIL_PAIR
+#define SVO_CEIL_PAIR 1    // both ceiling levels loaded without a branch between them (A/B: 0)
+#endif
 #ifndef SVO_CEIL_GATE
 #define SVO_CEIL_GATE 0    // A/B: 1 gates the ceiling box exits by a ballot in the primary instances too
 #endif
@@ -929,16 +932,24 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = P.ceil_sh[0], rows0 = (wm + 1u) >> lsh0;
             const uint32_t lsh1 = P.ceil_sh[1], rows1 = (wm + 1u) >> lsh1;
-            const uint32_t key = (w[2] >> lsh0) * rows0 + (w[0] >> lsh0);
+            const uint32_t key = __umul24(w[2] >> lsh0, rows0) + (w[0] >> lsh0);  // (< 2^28: 2^14 x 2^14 blocks at most)
 #if SVO_CEIL_CACHE
-            // (the lane's block and its ceilings stay in registers until it moves to another 64-column block)
+            // (the lane's block and its ceilings stay in registers until it moves to another block)
             if (key != ckey) {
                 ckey = key;
+#if SVO_CEIL_PAIR
+                // both ceilings loaded back to back, one wait (set_ceilings makes level 1 a copy of level 0 when
+                // the tree has one level)
+                const uint32_t k1 = __umul24(w[2] >> lsh1, rows1) + (w[0] >> lsh1);
+                const int16_t a0 = P.ceil[P.ceil_off[0] + (int64_t)key], a1 = P.ceil[P.ceil_off[1] + (int64_t)k1];
+                cval = (uint32_t)(uint16_t)a0 | ((uint32_t)(int32_t)a1 << 16);
+#else
                 int32_t c1 = 32767;
                 if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
                     c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
                 }
                 cval = ((uint32_t)(uint16_t)P.ceil[P.ceil_off[0] + (int64_t)key]) | ((uint32_t)c1 << 16);
+#endif
             }
             c0 = (int32_t)(int16_t)(cval & 0xFFFFu);
             c1 = (int32_t)cval >> 16;
@@ -1710,8 +1721,10 @@ static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& 
     P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
     P.ceil_levels = t->ceil_levels > lv[1] ? 2 : (t->ceil_levels > lv[0] ? 1 : 0);
     for (int j = 0; j < 2; j++) {
-        P.ceil_sh[j] = 2u * (uint32_t)(kCeilK0 + lv[j]);
-        P.ceil_off[j] = t->ceil_off[lv[j]];
+        // (one level only: the second is a copy of the first, so the kernel may read both unconditionally)
+        const int l = j < P.ceil_levels ? lv[j] : lv[0];
+        P.ceil_sh[j] = 2u * (uint32_t)(kCeilK0 + l);
+        P.ceil_off[j] = t->ceil_off[l];
     }
 }
 
