@@ -94,6 +94,7 @@ struct CastParams {
     int32_t ceil_levels;
     uint32_t ceil_sh[2];
     int64_t ceil_off[2];
+    const uint32_t* ceilp;  // the launch's two levels paired (svo_tree.d_ceilp at its first level's offset)
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
@@ -102,6 +103,9 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #endif
 #ifndef SVO_CEIL_CACHE
 #define SVO_CEIL_CACHE 1   // keep the lane's block ceilings in registers until it changes block (A/B: 0 loads them every iteration)
+#endif
+#ifndef SVO_CEIL_PACKED
+#define SVO_CEIL_PACKED 1  // both levels from one 32-bit load of the paired table (A/B: 0, two 16-bit loads)
 #endif
 #ifndef SVO_CEIL_PAIR
 #define SVO_CEIL_PAIR 1    // both ceiling levels loaded without a branch between them (A/B: 0)
@@ -927,17 +931,20 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         // per-lane path at the depth the moves since the last lookup left intact)
         int32_t cex[3] = {0, 0, 0};
         bool cl = false, any_cl = false;
-        int32_t c0 = -1, c1 = 32767;  // the ceilings of the lane's 64- and 256-column blocks
+        int32_t c0 = -1, c1 = 32767;  // the ceilings of the lane's blocks at the launch's two levels (set_ceilings)
         if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = P.ceil_sh[0], rows0 = (wm + 1u) >> lsh0;
-            const uint32_t lsh1 = P.ceil_sh[1], rows1 = (wm + 1u) >> lsh1;
+            [[maybe_unused]] const uint32_t lsh1 = P.ceil_sh[1], rows1 = (wm + 1u) >> lsh1;
             const uint32_t key = __umul24(w[2] >> lsh0, rows0) + (w[0] >> lsh0);  // (< 2^28: 2^14 x 2^14 blocks at most)
 #if SVO_CEIL_CACHE
             // (the lane's block and its ceilings stay in registers until it moves to another block)
             if (key != ckey) {
                 ckey = key;
-#if SVO_CEIL_PAIR
+#if SVO_CEIL_PACKED
+                // both ceilings in one load (svo_tree.d_ceilp: the block's ceiling and its parent block's)
+                cval = P.ceilp[key];
+#elif SVO_CEIL_PAIR
                 // both ceilings loaded back to back, one wait (set_ceilings makes level 1 a copy of level 0 when
                 // the tree has one level)
                 const uint32_t k1 = __umul24(w[2] >> lsh1, rows1) + (w[0] >> lsh1);
@@ -1720,6 +1727,8 @@ static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& 
     if (d->flags & SVO_CAST_NO_CEILINGS) return;
     P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
     P.ceil_levels = t->ceil_levels > lv[1] ? 2 : (t->ceil_levels > lv[0] ? 1 : 0);
+    // (the pair table of level lv[0] holds lv[0] + 1 = lv[1] when the tree has it, else lv[0] itself — as below)
+    P.ceilp = P.ceil_levels > 0 ? reinterpret_cast<const uint32_t*>(t->d_ceilp) + t->ceilp_off[lv[0]] : nullptr;
     for (int j = 0; j < 2; j++) {
         // (one level only: the second is a copy of the first, so the kernel may read both unconditionally)
         const int l = j < P.ceil_levels ? lv[j] : lv[0];
@@ -1807,7 +1816,8 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_pick) (void)hipFree(t->d_pick);
     if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
     if (t->d_ceil) (void)hipFree(t->d_ceil);
-    t->d_ceil = nullptr;
+    if (t->d_ceilp) (void)hipFree(t->d_ceilp);
+    t->d_ceil = t->d_ceilp = nullptr;
     t->ceil_levels = 0;
     t->d_ao_plan = nullptr;
     t->ao_plan_steps = -1;
@@ -1830,13 +1840,27 @@ static int upload_ceilings(svo_tree* t) {
     int64_t off[kCeilMax] = {0, 0, 0, 0};
     const int32_t n = tree_ceilings(t, c, off);
     if (t->d_ceil) (void)hipFree(t->d_ceil);
-    t->d_ceil = nullptr;
+    if (t->d_ceilp) (void)hipFree(t->d_ceilp);
+    t->d_ceil = t->d_ceilp = nullptr;
     t->ceil_levels = 0;
     if (n == 0) return SVO_OK;
+    // the pairs (level j, its parent block's level j+1; the last level paired with itself)
+    std::vector<uint32_t> pc(c.size());
+    for (int32_t j = 0; j < n; j++) {
+        const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
+        const int32_t up = j + 1 < n ? j + 1 : j, sh = up > j ? 2 : 0;
+        const int64_t rows_up = rows >> sh;
+        for (int64_t z = 0; z < rows; z++)
+            for (int64_t x = 0; x < rows; x++)
+                pc[off[j] + z * rows + x] = (uint32_t)(uint16_t)c[off[j] + z * rows + x] |
+                                            ((uint32_t)(uint16_t)c[off[up] + (z >> sh) * rows_up + (x >> sh)] << 16);
+    }
     HIP_TRY(hipMalloc(&t->d_ceil, c.size() * sizeof(int16_t)), SVO_ENOMEM);
     HIP_TRY(hipMemcpy(t->d_ceil, c.data(), c.size() * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    HIP_TRY(hipMalloc(&t->d_ceilp, pc.size() * sizeof(uint32_t)), SVO_ENOMEM);
+    HIP_TRY(hipMemcpy(t->d_ceilp, pc.data(), pc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     t->ceil_levels = n;
-    for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = off[j];
+    for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = t->ceilp_off[j] = off[j];
     return SVO_OK;
 }
 

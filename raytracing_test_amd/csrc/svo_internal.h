@@ -76,6 +76,10 @@ struct svo_tree {
     void* d_ceil = nullptr;
     int32_t ceil_levels = 0;
     int64_t ceil_off[4] = {0, 0, 0, 0};
+    // the same ceilings paired for one-load reads: for every block of level j, its ceiling (low 16 bits) and that of
+    // its level-(j+1) block (high 16 bits; the last level repeats its own), uint32 at element ceilp_off[j] of d_ceilp
+    void* d_ceilp = nullptr;
+    int64_t ceilp_off[4] = {0, 0, 0, 0};
 };
 
 namespace svo {
