@@ -107,6 +107,9 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #ifndef SVO_CEIL_PACKED
 #define SVO_CEIL_PACKED 1  // both levels from one 32-bit load of the paired table (A/B: 0, two 16-bit loads)
 #endif
+#ifndef SVO_BOX_GATE
+#define SVO_BOX_GATE 1     // forward boxes skipped when every crossing lane of the wave takes a ceiling box (A/B: 0)
+#endif
 #ifndef SVO_CEIL_PAIR
 #define SVO_CEIL_PAIR 1    // both ceiling levels loaded without a branch between them (A/B: 0)
 #endif
@@ -999,11 +1002,26 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         } else if (!(fast && [&] {
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
+#if SVO_BOX_GATE
+                       // (a wave whose every crossing is a ceiling move — the air above the terrain — skips the forward
+                       // boxes: wave-uniform)
+                       if (!any_cl || __ballot(!cl) != 0ull) {
+                           box_exits(w, R.s, sh, par.mask, ud, ex);
+                           if (any_cl) {
+#pragma unroll
+                               for (int k = 0; k < 3; k++) ex[k] = cl ? cex[k] : ex[k];
+                           }
+                       } else {
+#pragma unroll
+                           for (int k = 0; k < 3; k++) ex[k] = cex[k];
+                       }
+#else
                        box_exits(w, R.s, sh, par.mask, ud, ex);
                        if (any_cl) {
 #pragma unroll
                            for (int k = 0; k < 3; k++) ex[k] = cl ? cex[k] : ex[k];
                        }
+#endif
                        const bool moved_ok = skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                        if (ceil_on && cl && moved_ok) {
                            // (the voxel this move started from need not lie in the parent's region: the step
