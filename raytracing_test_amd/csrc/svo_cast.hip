@@ -114,7 +114,7 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 #define SVO_CEIL_PAIR 1    // both ceiling levels loaded without a branch between them (A/B: 0)
 #endif
 #ifndef SVO_CEIL_GATE
-#define SVO_CEIL_GATE 0    // A/B: 1 gates the ceiling box exits by a ballot in the primary instances too
+#define SVO_CEIL_GATE 1    // the ceiling box exits computed only when a lane of the wave is above its ceiling (A/B: 0, per-lane selects)
 #endif
 #ifndef SVO_PRIO_TOP
 #define SVO_PRIO_TOP 0     // A/B: tile rows from the top whose waves raise their issue priority
@@ -972,8 +972,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             const bool p1 = y > c1;
             cl = p1 || y > c0;
         }
-        // (the shading instances take the box exits only when a lane of the wave moves — wave-uniform; the
-        // primary ones select them per lane; the two measured equal within 1 %: profiles/r03/ab_f_*.log, ab_g_*.log)
+        // (the box exits are taken only when a lane of the wave moves — wave-uniform; with the forward boxes gated
+        // the same way, 1.1 % faster at C3 than per-lane selects: profiles/r03/ab_r03_x_*.log)
         any_cl = ceil_on && ((!REFLECT && !SVO_CEIL_GATE) || __ballot(cl) != 0ull);
         if (any_cl) {
             const int32_t y = (int32_t)w[1];
