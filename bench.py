@@ -7,14 +7,19 @@ normalize(1,-0.45,1), step budget 16384, castRayFromCam semantics (every ray end
 Other configs: --config c1 (dense 256^3 grid, 256^2 rays), c2 / c2cam0 (the reference world), c2d8 (genWorld in a depth-8 tree),
 c5 (depth-14, 4K); --ao N (C4: + N hemisphere AO rays per hit); --shade (the shading pass).
 
-A "step" = one pass of the cast kernel over the step's frames.  Multi-GPU (one process per GPU,
-torch.distributed.run): frames are sharded by interleaved 8-pixel tile rows (row r -> rank r mod N)
+A "step" = one pass of the cast kernel over the step's frames.  Multi-GPU: one process per GPU, either
+under a launcher (torch.distributed.run ... bench.py --gpus N; WORLD_SIZE must equal N) or started by
+bench.py itself (`python bench.py --gpus N` with no WORLD_SIZE: N child processes, RANK = LOCAL_RANK =
+r, before anything touches a GPU; rank 0 prints the line, the exit status is the first failing
+rank's).  `n_gpus` on the line is the size of the communicator the step ran over (svo_exchange_info
+for the RCCL exchange).  Frames are sharded by interleaved 8-pixel tile rows (row r -> rank r mod N)
 and every frame's shards are gathered over RCCL to the rank that displays it, by the C ABI's
 svo_exchange_frames (include/svo_rt.h), overlapped with the next step's cast on a second stream.
   * default ("weak"): a step renders N frames (camera poses shifted along the diagonal), so per-GPU
     work is fixed as N grows; frame f is displayed by rank f (the gathers form one all-to-all);
   * --frames F ("strong"): a step renders F frames whatever N is (C5 as BASELINE.json words it:
-    --config c5 --frames 1 = one 4K frame split over N GPUs, gathered to rank 0).
+    --config c5 --frames 1 = one 4K frame split over N GPUs, gathered to rank 0:
+    `python bench.py --gpus 8 --config c5 --frames 1`).
 Inputs (tree, camera) are resident in HBM before the timed region; the timed region is K steps
 between barrier + synchronize on both sides; the reported time is the max over ranks.
 
@@ -308,6 +313,60 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
     return roof
 
 
+# ------------------------------------------------------------------------------ rank launcher --
+def _free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, grace_s=30.0, script=None):
+    """`python bench.py --gpus N` without a launcher: start N fresh child processes of this script, one
+    per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port), and wait
+    for them.  This process touches no GPU (nothing here imports torch), and nothing is exec'd: the
+    children are new processes.  Rank 0 prints the JSON line on the inherited stdout.  When a child
+    fails, the others get `grace_s` to finish before they are terminated (by PID); the exit status is
+    the first failing child's (a signal: 128 + its number)."""
+    import signal
+    import subprocess
+
+    env0 = dict(os.environ)
+    env0.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                GROUP_RANK="0", ROLE_RANK="0", TORCHELASTIC_RUN_ID="bench_%d" % os.getpid())
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), ROLE_WORLD_SIZE=str(n))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc, t_fail = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        for c in codes:
+            if c is not None and c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                t_fail = time.monotonic()
+        if all(c is not None for c in codes):
+            break
+        if t_fail is not None and time.monotonic() - t_fail > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+            t_kill = time.monotonic()
+            while any(p.poll() is None for p in procs) and time.monotonic() - t_kill < 10.0:
+                time.sleep(0.1)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.05)
+    if rc:
+        print("bench.py: a rank failed (exit status %d); see its stderr" % rc, file=sys.stderr)
+    return rc
+
+
 # ------------------------------------------------------------------------------------- main --
 def main():
     ap = argparse.ArgumentParser()
@@ -345,6 +404,14 @@ def main():
                     help="an event pair around every cast launch (default at N=1: one pair around the timed region, whose "
                          "average per launch includes the gaps between launches; per-launch pairs cost ~7 us per step)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher around us: start the ranks ourselves, before anything touches a GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        ap.error("WORLD_SIZE=%s (from the launcher) differs from --gpus %d" % (env_world, args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -355,7 +422,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and world > ndev:
+        ap.error("%d ranks over RCCL need %d GPUs (%d visible); --dist-backend gloo rehearses N ranks on fewer" % (world, world, ndev))
+    dev = local % max(1, ndev)
     torch.cuda.set_device(dev)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -460,6 +530,8 @@ def main():
             else:
                 uid = rt.Exchange.unique_id()
             exch = rt.Exchange(world, rank, uid, dev)
+            if exch.info() != (rank, world):
+                raise RuntimeError("svo_exchange_info reports rank/size %s, expected (%d, %d)" % (exch.info(), rank, world))
         except rt.SvoError as e:  # keep the scaling run alive; say so on the line
             xmode, xnote = "torch", "svo_exchange_create failed (%s); torch.distributed all_to_all used" % e
         if exch is not None and n_own:
@@ -595,6 +667,9 @@ def main():
     if args.stats and rank == 0:
         print_stats(rt, tree, desc, outs[0], stream, torch)
 
+    # the job's size as the communicators report it: the C-ABI exchange's RCCL communicator
+    # (svo_exchange_info), else the torch.distributed group
+    n_gpus = exch.info()[1] if exch is not None else (dist.get_world_size() if world > 1 else 1)
     if exch is not None:  # the RCCL communicator of the exchange goes before the process group's
         torch.cuda.synchronize()
         exch.close()
@@ -622,7 +697,7 @@ def main():
         "metric": metric,
         "value": round(value, 1),
         "unit": "rays/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),

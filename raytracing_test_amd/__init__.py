@@ -729,6 +729,12 @@ class Exchange:
             _lib.svo_exchange_destroy(self._h)
             self._h = None
 
+    def info(self):
+        """(rank, nranks) of the exchange's RCCL communicator (svo_exchange_info)."""
+        r, n = C.c_int32(), C.c_int32()
+        _check(lib().svo_exchange_info(self._h, C.byref(r), C.byref(n)), "svo_exchange_info")
+        return r.value, n.value
+
     def frames(self, tree, desc, mine, frames_out, stream=None):
         """One step's exchange of `mine` (this rank's shard of desc's frames) into frames_out (the
         whole frames this rank displays), asynchronous on `stream`."""

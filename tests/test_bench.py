@@ -96,3 +96,48 @@ def test_torch_exchange_splits_pair_up(bench, world, nframes):
     for s in range(world):
         for r in range(world):
             assert send[s][r] == recv[r][s], (s, r)
+
+
+# ---- the launcher-free N-rank start (`python bench.py --gpus N` with no WORLD_SIZE) ----
+_CHILD = r'''
+import os, sys, time
+r, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+assert os.environ["LOCAL_RANK"] == str(r) and os.environ["MASTER_ADDR"] == "127.0.0.1" and int(os.environ["MASTER_PORT"]) > 0
+mode = sys.argv[1]
+if mode == "ok":
+    if r == 0:
+        print('{"n": %d, "args": "%s"}' % (n, " ".join(sys.argv[1:])), flush=True)
+    sys.exit(0)
+if mode == "fail":  # rank 1 fails at once, the others would wait forever (a barrier that never completes)
+    if r == 1:
+        sys.exit(3)
+    time.sleep(600)
+'''
+
+
+def test_launch_ranks_starts_n_children(bench, tmp_path, capfd):
+    child = tmp_path / "child.py"
+    child.write_text(_CHILD)
+    assert bench.launch_ranks(3, ["ok", "--x"], script=str(child)) == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    assert out == ['{"n": 3, "args": "ok --x"}']  # rank 0's line only
+
+
+def test_launch_ranks_failure_ends_the_job(bench, tmp_path):
+    import time
+
+    child = tmp_path / "child.py"
+    child.write_text(_CHILD)
+    t0 = time.monotonic()
+    assert bench.launch_ranks(3, ["fail"], grace_s=1.0, script=str(child)) == 3  # the failing rank's status
+    assert time.monotonic() - t0 < 30  # the waiting ranks were terminated, not waited for
+
+
+def test_world_size_must_match_gpus(monkeypatch):
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert p.returncode == 2 and "differs from --gpus" in p.stderr

@@ -42,3 +42,22 @@ def test_strong_two_frames_verified():
     d = _run(29613, "--frames", "2")
     assert d["scaling"] == "strong"
     assert d["gather_verified"] is True, d
+
+
+def test_launcher_free_two_ranks_verified():
+    """`python bench.py --gpus 2` with no launcher: bench.py starts the two ranks itself (before any GPU call),
+    and the line reports the communicator's size"""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--steps", "2", "--warmup", "1",
+           "--verify", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0's line only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["gather_verified"] is True, d
