@@ -98,39 +98,11 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
-#ifndef SVO_CEIL_LEVELS
-#define SVO_CEIL_LEVELS 2  // column-ceiling levels the traversal checks: 64-column blocks, then 256 (A/B: 1)
-#endif
-#ifndef SVO_CEIL_CACHE
-#define SVO_CEIL_CACHE 1   // keep the lane's block ceilings in registers until it changes block (A/B: 0 loads them every iteration)
-#endif
-#ifndef SVO_CEIL_PACKED
-#define SVO_CEIL_PACKED 1  // both levels from one 32-bit load of the paired table (A/B: 0, two 16-bit loads)
-#endif
-#ifndef SVO_BOX_GATE
-#define SVO_BOX_GATE 1     // forward boxes skipped when every crossing lane of the wave takes a ceiling box (A/B: 0)
-#endif
-#ifndef SVO_CEIL_PAIR
-#define SVO_CEIL_PAIR 1    // both ceiling levels loaded without a branch between them (A/B: 0)
-#endif
-#ifndef SVO_CEIL_GATE
-#define SVO_CEIL_GATE 1    // the ceiling box exits computed only when a lane of the wave is above its ceiling (A/B: 0, per-lane selects)
-#endif
-#ifndef SVO_PRIO_TOP
-#define SVO_PRIO_TOP 0     // A/B: tile rows from the top whose waves raise their issue priority
-#endif
-#ifndef SVO_DROP_TOP
-#define SVO_DROP_TOP 0     // diagnostics only (A/B of the critical path): the top tile rows cast nothing
-#endif
-#ifndef SVO_ITER_CAP
-#define SVO_ITER_CAP 0     // diagnostics only: rays still running after this many traversal iterations stop (steps_left -1)
-#endif
-#ifndef SVO_SHADE_WAVES
-#define SVO_SHADE_WAVES 8  // waves per SIMD the shading instances are held to (A/B: 7 fits them without spills)
-#endif
-#ifndef SVO_XCD_GROUP
-#define SVO_XCD_GROUP 0  // A/B: footprints grouped per XCD (see k_cast)
-#endif
+// (round 3's A/B switches — ceiling caching and packing, wave-gated boxes, XCD grouping, issue priority —
+// were resolved to their measured winners and removed from the source; the losing sides are in git history
+// (DESIGN.md cites the commits) and build_variant.py --rev rebuilds them.  The critical-path diagnostics
+// (an iteration cap, dropping the top tile rows) are patches: tools/variants/*.patch, build_variant.py --patch)
+constexpr int kShadeWaves = 8;  // waves per SIMD the shading instances are held to (7 fits them without spills: 4 % slower)
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -896,25 +868,13 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
     const bool ceil_on = CEIL && P.ceil_levels > 0;  // (uniform)
-#if SVO_CEIL_CACHE
-    uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 64-column block (key) and its ceilings (c0 | c1 << 16)
-#endif
-#if SVO_ITER_CAP > 0
-    int32_t iters = 0;
-    bool capped = false;
-#endif
+    uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 16-column block (key) and its ceilings (c0 | c1 << 16)
     while (!done) {
         // the voxel just entered is untested
         if (STATS) {
             st.wv_iters += wave_lead();
             st.iters++;
         }
-#if SVO_ITER_CAP > 0
-        if (++iters > SVO_ITER_CAP) {
-            capped = true;
-            break;
-        }
-#endif
         const int32_t steps_in = R.steps;  // (the progress guard below)
         uint32_t w[3];
         wrap3(R, wm, w);
@@ -938,43 +898,21 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = P.ceil_sh[0], rows0 = (wm + 1u) >> lsh0;
-            [[maybe_unused]] const uint32_t lsh1 = P.ceil_sh[1], rows1 = (wm + 1u) >> lsh1;
             const uint32_t key = __umul24(w[2] >> lsh0, rows0) + (w[0] >> lsh0);  // (< 2^28: 2^14 x 2^14 blocks at most)
-#if SVO_CEIL_CACHE
-            // (the lane's block and its ceilings stay in registers until it moves to another block)
+            // (the lane's block and its ceilings stay in registers until it moves to another block; both
+            // ceilings come from one 32-bit load of svo_tree.d_ceilp: the block's ceiling and its parent block's)
             if (key != ckey) {
                 ckey = key;
-#if SVO_CEIL_PACKED
-                // both ceilings in one load (svo_tree.d_ceilp: the block's ceiling and its parent block's)
                 cval = P.ceilp[key];
-#elif SVO_CEIL_PAIR
-                // both ceilings loaded back to back, one wait (set_ceilings makes level 1 a copy of level 0 when
-                // the tree has one level)
-                const uint32_t k1 = __umul24(w[2] >> lsh1, rows1) + (w[0] >> lsh1);
-                const int16_t a0 = P.ceil[P.ceil_off[0] + (int64_t)key], a1 = P.ceil[P.ceil_off[1] + (int64_t)k1];
-                cval = (uint32_t)(uint16_t)a0 | ((uint32_t)(int32_t)a1 << 16);
-#else
-                int32_t c1 = 32767;
-                if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
-                    c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
-                }
-                cval = ((uint32_t)(uint16_t)P.ceil[P.ceil_off[0] + (int64_t)key]) | ((uint32_t)c1 << 16);
-#endif
             }
             c0 = (int32_t)(int16_t)(cval & 0xFFFFu);
             c1 = (int32_t)cval >> 16;
-#else
-            c0 = P.ceil[P.ceil_off[0] + (int64_t)key];
-            if (SVO_CEIL_LEVELS > 1 && P.ceil_levels > 1) {  // (uniform)
-                c1 = P.ceil[P.ceil_off[1] + (int64_t)(w[2] >> lsh1) * rows1 + (w[0] >> lsh1)];
-            }
-#endif
             const bool p1 = y > c1;
             cl = p1 || y > c0;
         }
         // (the box exits are taken only when a lane of the wave moves — wave-uniform; with the forward boxes gated
         // the same way, 1.1 % faster at C3 than per-lane selects: profiles/r03/ab_r03_x_*.log)
-        any_cl = ceil_on && ((!REFLECT && !SVO_CEIL_GATE) || __ballot(cl) != 0ull);
+        any_cl = ceil_on && __ballot(cl) != 0ull;
         if (any_cl) {
             const int32_t y = (int32_t)w[1];
             const bool p1 = y > c1;
@@ -1002,7 +940,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         } else if (!(fast && [&] {
                        int32_t ex[3];
                        if (REFLECT) dir_flags(R.s, ud);  // reflections and refractions flip steps
-#if SVO_BOX_GATE
                        // (a wave whose every crossing is a ceiling move — the air above the terrain — skips the forward
                        // boxes: wave-uniform)
                        if (!any_cl || __ballot(!cl) != 0ull) {
@@ -1015,13 +952,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
 #pragma unroll
                            for (int k = 0; k < 3; k++) ex[k] = cex[k];
                        }
-#else
-                       box_exits(w, R.s, sh, par.mask, ud, ex);
-                       if (any_cl) {
-#pragma unroll
-                           for (int k = 0; k < 3; k++) ex[k] = cl ? cex[k] : ex[k];
-                       }
-#endif
                        const bool moved_ok = skip_box<TRACK, RB>(R, ex, REFLECT ? SEG && __ballot(!lin) != 0ull : wseg);
                        if (ceil_on && cl && moved_ok) {
                            // (the voxel this move started from need not lie in the parent's region: the step
@@ -1182,9 +1112,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // (out of the loop, so the stepping loop's state copies stay off every skip, and the lanes
     // whose budget ends in empty space take their last steps together).  Every other way out of
     // the loop without a hit has spent the budget.
-#if SVO_ITER_CAP > 0
-    if (capped) escaped = true;
-#endif
     if (!hit && !escaped) {
         while (R.steps > 0) {
             dda_step(R);
@@ -1235,9 +1162,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     h.y = R.r[1];
     h.z = R.r[2];
     h.steps_left = hit ? R.steps : 0;
-#if SVO_ITER_CAP > 0
-    if (capped) h.steps_left = -1;
-#endif
     h.t = (float)R.tlast;  // (one rounding of the same double as before)
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
@@ -1362,7 +1286,7 @@ template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
 // with a 12-byte spill (2.9 % faster than 6 waves)
-__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVES : 8)) void k_cast(const CastParams P) {
+__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1379,16 +1303,6 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
     int64_t blk = blockIdx.x;
-#if SVO_XCD_GROUP > 0
-    if (P.mode == MODE_FRAME) {
-        // blocks are dealt round-robin to the 8 XCDs (b and b + 8 share an L2): within every run of
-        // 8 * G blocks, XCD x takes the G consecutive footprints x*G .. x*G + G-1, so the footprints one L2
-        // serves are neighbours (the load stays balanced: every XCD takes its share of every run)
-        constexpr int64_t G = SVO_XCD_GROUP;
-        const int64_t nb = gridDim.x, k = blk >> 3, run = k / G, base = run * 8 * G;
-        if (base + 8 * G <= nb) blk = base + (blk & 7) * G + (k - run * G);
-    }
-#endif
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
@@ -1407,10 +1321,6 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
         // them first keeps the long tiles out of the launch's tail)
         if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
-#if SVO_PRIO_TOP > 0
-        // A/B: the top tile rows (the launch's longest waves, dispatched first) win issue arbitration
-        if (trl >= P.tile_rows_local - SVO_PRIO_TOP) __builtin_amdgcn_s_setprio(3);
-#endif
         const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
         const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
         // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
@@ -1418,7 +1328,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? SVO_SHADE_WAVE
         const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
         const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
         const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-        if (trl >= 0 && trl < P.tile_rows_local - SVO_DROP_TOP && px < P.width && py < P.height) {
+        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
             raygen_pixel(P.rg, px, py, d);
             o[0] = P.frame_org[3 * fr + 0];
             o[1] = P.frame_org[3 * fr + 1];

@@ -1,5 +1,8 @@
-"""Build libsvo_rt.so from another git revision (or the working tree with -D defines) into variants/
-for A/B timing:  python tools/build_variant.py <name> [--rev REV] [-D NAME=VAL ...]"""
+"""Build libsvo_rt.so from another git revision (or the working tree with -D defines and / or patches)
+into variants/ for A/B timing:
+    python tools/build_variant.py <name> [--rev REV] [--patch tools/variants/X.patch ...] [-D NAME=VAL ...]
+The product source carries no experiment switches: A/B losers are rebuilt from the revision that had
+them (--rev), diagnostics (tools/variants/*.patch) from a patched copy of the sources."""
 import argparse
 import os
 import shutil
@@ -15,13 +18,20 @@ def main():
     ap.add_argument("name")
     ap.add_argument("--rev", default=None)
     ap.add_argument("-D", action="append", default=[])
+    ap.add_argument("--patch", action="append", default=[], help="a unified diff against the source tree (tools/variants/*.patch)")
     ap.add_argument("--flag", action="append", default=[], help="extra hipcc flags, space-separated (e.g. '-mllvm -amdgpu-sched-strategy=max-ilp')")
     a = ap.parse_args()
     src_root = ROOT
     tmp = None
-    if a.rev:
+    if a.rev or a.patch:
         tmp = tempfile.mkdtemp()
-        subprocess.check_call("git -C %s archive %s raytracing_test_amd include | tar -x -C %s" % (ROOT, a.rev, tmp), shell=True)
+        if a.rev:
+            subprocess.check_call("git -C %s archive %s raytracing_test_amd include | tar -x -C %s" % (ROOT, a.rev, tmp), shell=True)
+        else:
+            for d in ("raytracing_test_amd", "include"):
+                shutil.copytree(os.path.join(ROOT, d), os.path.join(tmp, d), ignore=shutil.ignore_patterns("_build", "*.so", "__pycache__"))
+        for pf in a.patch:
+            subprocess.check_call(["git", "apply", "--unsafe-paths", "--directory=.", os.path.abspath(pf)], cwd=tmp)
         src_root = tmp
     sys.path.insert(0, os.path.join(src_root, "raytracing_test_amd"))
     import build  # noqa
