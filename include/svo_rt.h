@@ -157,14 +157,20 @@ int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* xyz, int64_t
    after a rebuild / when the device allocation is outgrown) */
 int svo_tree_sync(svo_tree* t);
 void svo_tree_destroy(svo_tree* t);
+/* The column ceilings the casts use (SVO_CAST_NO_CEILINGS): for k = SVO_CEIL_K0 .. min(levels - 1, SVO_CEIL_K0 + 3)
+   (blocks of 16, 64, 256 and 1024 columns), per aligned block of 4^k x 4^k columns, the highest stored voxel row of
+   the tree in those columns (-1: none), row-major [z][x], level after level (finest first; level j's blocks are
+   4^(SVO_CEIL_K0 + j) columns wide).  out may be NULL (count only); levels = number of levels, n = elements. */
+#define SVO_CEIL_K0 2
+int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n);
+/* The column-ceiling tables in HBM as the casts read them (inspection / tests): the int16 ceilings in
+   svo_tree_ceilings' layout and their uint32 pairs (low: the block's ceiling, high: its next-level block's; the
+   last level paired with itself).  levels = 0 when the tree has none.  Either buffer may be NULL. */
+int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32_t* pairs, int64_t cap, int32_t* levels, int64_t* n);
 /* Checkpoint (the reference regenerates its world at every start, main.cpp:190): write the
    linearised tree (levels, view, palette, nodes, material runs; a checksum) to `path`, and read it back
    as a new tree (not uploaded).  Loading validates every child / material reference against the array
    sizes, so a damaged file fails with SVO_EIO instead of reaching a kernel. */
-/* The column ceilings the casts use (SVO_CAST_NO_CEILINGS): for k = 3 .. min(levels - 1, 6), per aligned block of
-   4^k x 4^k columns, the highest stored voxel row of the tree in those columns (-1: none), row-major [z][x],
-   level after level (finest first).  out may be NULL (count only); levels = number of levels, n = elements. */
-int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n);
 int svo_tree_save(const svo_tree* t, const char* path);
 int svo_tree_load(const char* path, svo_tree** out);
 
@@ -259,9 +265,10 @@ typedef struct {
 /* svo_cast_desc.flags (results identical): frames whose rays all step with the same signs run an
    instance with those signs compiled in; this bit keeps the per-wave sign flags instead */
 #define SVO_CAST_NO_OCTANT 16384
-/* svo_cast_desc.flags (results identical): rays above the highest stored row of the 256- or 64-column block
-   they are in cross the empty box above that row in one move, without a tree lookup (column ceilings,
-   computed at upload / sync); this bit walks the tree instead */
+/* svo_cast_desc.flags (results identical): rays above the highest stored row of the column block they are in
+   (primary casts: 16- and 64-column blocks; the shading pass: 64 and 256) cross the empty box above that row in
+   one move, without a tree lookup (column ceilings, svo_tree_ceilings, computed at upload / sync); this bit walks
+   the tree instead */
 #define SVO_CAST_NO_CEILINGS 32768
 
 /* number of rays a desc produces on this shard (= records written) */
@@ -273,6 +280,10 @@ int svo_cast_rays(const svo_tree* t, const svo_cast_desc* d, const svo_hits* out
 /* RAY_CASTER::castRayFromCam with explicit camera (synchronous, one ray on the GPU) */
 int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* out,
                           svo_block* block);
+/* Launches over t whose rays ended on the traversal's progress guard (an iteration that took no DDA step:
+   only a wrong crossing count can cause it).  Such a ray's record has stepsLeft = -1 and no hit; the count
+   should be 0.  reset != 0 zeroes the counter.  Synchronous (reads device memory). */
+int svo_tree_guard_trips(const svo_tree* t, uint64_t* trips, int32_t reset);
 int svo_sync(void* hip_stream);
 
 /* Wire formats of hit records for the exchange between GPUs (the tile-row gather):

@@ -46,10 +46,11 @@ STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "bric
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
               "no_progress", "root_starts", "cache_empty", "wave_skips", "wave_descents",
-              "path_starts", "ao_node_loads", "ceil_moves")  # wave_*: per wave (64 rays)
+              "path_starts", "ao_node_loads", "ceil_moves", "iters_above_top", "bends")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: the larger wire record (12 B general, 8 B compact: Tree.wire_bytes(desc))
+CEIL_K0 = 2  # SVO_CEIL_K0: the finest column-ceiling blocks are 4^2 = 16 columns wide
 VIEW_SOLID, VIEW_ALL = 0, 1  # SVO_VIEW_*: castRayFromCam's blocks / every stored block (the shading scene)
 
 
@@ -140,6 +141,7 @@ ABI_SYMBOLS = (
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
+    "svo_tree_guard_trips", "svo_tree_device_ceilings",
 )
 
 
@@ -179,7 +181,9 @@ def lib():
                      ("svo_wire_bytes", [vp, C.POINTER(CastDesc), C.POINTER(i32)]), ("svo_cast_wire", [vp, C.POINTER(CastDesc), vp, vp, vp]),
                      ("svo_wire_scatter", [vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
                      ("svo_exchange_wire", [vp, vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
-                     ("svo_tree_ceilings", [vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)])):
+                     ("svo_tree_ceilings", [vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
+                     ("svo_tree_guard_trips", [vp, C.POINTER(C.c_uint64), i32]),
+                     ("svo_tree_device_ceilings", [vp, vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -554,14 +558,14 @@ class Tree:
         return out
 
     def ceilings(self):
-        """the column ceilings (svo_tree_ceilings): a list of (E / 4^k) x (E / 4^k) int16 arrays [z][x], k = k0, k0 + 1, ... (k0 = 3 unless built otherwise)"""
+        """the column ceilings (svo_tree_ceilings): a list of (E / 4^k) x (E / 4^k) int16 arrays [z][x], k = CEIL_K0, CEIL_K0 + 1, ..."""
         lv, n = C.c_int32(), C.c_int64()
         _check(lib().svo_tree_ceilings(self._h, None, 0, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
         out = np.zeros(n.value, np.int16)
         _check(lib().svo_tree_ceilings(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
         E = 1 << (2 * self.info().levels)
-        # the finest level's blocks are 4^k0 columns wide (SVO_CEIL_K0, 3 by default): the one k0 whose level sizes add up to n
-        k0 = next(k for k in range(1, 8) if sum((E >> (2 * (k + j))) ** 2 for j in range(lv.value)) == n.value) if lv.value else 3
+        k0 = CEIL_K0  # the finest level's blocks are 4^SVO_CEIL_K0 columns wide
+        assert sum((E >> (2 * (k0 + j))) ** 2 for j in range(lv.value)) == n.value
         self.ceil_k0 = k0
         res, off = [], 0
         for j in range(lv.value):
@@ -637,6 +641,41 @@ class Tree:
         _check(lib().svo_sync(None), "svo_sync")
         v = st[:len(STAT_NAMES)].cpu().numpy().astype(np.float64)
         return {k: v[i] / max(1.0, v[0]) for i, k in enumerate(STAT_NAMES)}
+
+    def device_ceilings(self):
+        """(levels, int16 ceilings, uint32 pairs) of the tables in HBM (svo_tree_device_ceilings)"""
+        lv, n = C.c_int32(), C.c_int64()
+        _check(lib().svo_tree_device_ceilings(self._h, None, None, 0, C.byref(lv), C.byref(n)), "svo_tree_device_ceilings")
+        c = np.zeros(n.value, np.int16)
+        p = np.zeros(n.value, np.uint32)
+        _check(lib().svo_tree_device_ceilings(self._h, c.ctypes.data_as(C.c_void_p), p.ctypes.data_as(C.c_void_p), n.value, C.byref(lv),
+                                              C.byref(n)), "svo_tree_device_ceilings")
+        return lv.value, c, p
+
+    def guard_trips(self, reset=False):
+        """Rays of launches over this tree that ended on the progress guard (svo_tree_guard_trips): 0 unless a
+        crossing count is wrong; such rays carry stepsLeft -1."""
+        v = C.c_uint64()
+        _check(lib().svo_tree_guard_trips(self._h, C.byref(v), 1 if reset else 0), "svo_tree_guard_trips")
+        return v.value
+
+    def shade_stats(self, origin, cam_dir, width, height, steps, scene=None, flags=0, shadow_steps=75, ray_work=False):
+        """Traversal counters of one shaded frame (SVO_CAST_STATS in the shading pass; the shadow rays' work is not
+        counted), per pixel: {STAT_NAMES[k]: value}; with ray_work, also the per-pixel packed work words (int64)."""
+        torch = _torch()
+        d = self.frame_desc(origin, cam_dir, width, height, steps, None, None, 0, 1, flags | CAST_STATS, 0, 5)
+        n = self.count(d)
+        dev = self.info().device
+        st = torch.zeros(STATS_HEADER + 2 * self.blocks(d) + n, dtype=torch.int64, device=torch.device("cuda", dev))
+        d.stats = st.data_ptr()
+        rgba = torch.empty((n, 4), dtype=torch.float32, device=torch.device("cuda", dev))
+        self.shade(d, rgba, shadow_steps=shadow_steps, scene=scene)
+        _check(lib().svo_sync(None), "svo_sync")
+        v = st[:len(STAT_NAMES)].cpu().numpy().astype(np.float64)
+        res = {k: v[i] / max(1.0, v[0]) for i, k in enumerate(STAT_NAMES)}
+        if ray_work:
+            res["ray_work"] = st[STATS_HEADER + 2 * self.blocks(d):].cpu().numpy()
+        return res
 
     def cast_rays(self, dirs, origins=None, steps=300, origin=(0.0, 0.0, 0.0), out=None, stream=None, sync=True, flags=0):
         """Explicit rays: dirs / origins are (n, 3) float32 device tensors."""

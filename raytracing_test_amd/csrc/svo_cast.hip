@@ -95,6 +95,7 @@ struct CastParams {
     uint32_t ceil_sh[2];
     int64_t ceil_off[2];
     const uint32_t* ceilp;  // the launch's two levels paired (svo_tree.d_ceilp at its first level's offset)
+    uint32_t* guard_trips;  // the tree's counter of progress-guard trips (svo_tree_guard_trips)
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
@@ -469,6 +470,8 @@ struct Stats {
     uint32_t no_progress;                          // loop iterations that consumed no budget (the guard's trips: 0)
     uint32_t ceil_moves;                           // crossings of a column-ceiling box (no lookup)
     uint32_t iters;                                // this lane's traversal iterations
+    uint32_t above_top;                            // iterations that start above the tree's highest stored row
+    uint32_t bends;                                // reflections and refractions (shading)
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -840,7 +843,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -878,6 +881,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         const int32_t steps_in = R.steps;  // (the progress guard below)
         uint32_t w[3];
         wrap3(R, wm, w);
+        if (STATS && pre_top >= 0 && (int32_t)w[1] > pre_top) st.above_top++;
         if (ESCAPE && top >= 0 && R.s[1] > 0 && (int32_t)w[1] > top && (int64_t)w[1] + R.steps <= (int64_t)wm) {
             escaped = true;  // only empty voxels ahead: a miss
             break;
@@ -1017,6 +1021,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                 }
             }
             bounce->n++;
+            if (STATS) st.bends++;
 #pragma unroll
             for (int k = 0; k < 3; k++) bounce->m[k] *= 0.94f;
             dda_step(R);
@@ -1037,6 +1042,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             wrap3(R, wm, wr);  // the refractive voxel (its region, when uniform, is passed below)
             if (!bounce->bent) {
                 bounce->bent = true;
+                if (STATS) st.bends++;
                 const uint32_t ax = R.axis;
                 double ex[3];
                 float nrm[3] = {0.0f, 0.0f, 0.0f};
@@ -1105,6 +1111,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         // 1a85dd6) — ends the ray: the launch always ends.  (STATS counts the trips: 0 in every test.)
         if (R.steps >= steps_in && !done) {
             if (STATS) st.no_progress++;
+            R.steps = -1;  // marked in every build: the record's steps_left is -1 and the tree's trip counter counts it
             done = true;
         }
     }
@@ -1145,6 +1152,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 21, (unsigned long long)st.path_starts);
         if (st.no_progress) atomicAdd(P.stats + 16, (unsigned long long)st.no_progress);
         atomicAdd(P.stats + 23, (unsigned long long)st.ceil_moves);
+        atomicAdd(P.stats + 24, (unsigned long long)st.above_top);
+        atomicAdd(P.stats + 25, (unsigned long long)st.bends);
         // per-ray work (offline analysis, bench.py SVO_RAY_WORK): 16-bit fields, lookups | iterations | brick steps | node loads
         if (ray_work)
             *ray_work = (unsigned long long)min(st.lookups, 65535u) | ((unsigned long long)min(st.iters, 65535u) << 16) |
@@ -1161,7 +1170,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     h.x = R.r[0];
     h.y = R.r[1];
     h.z = R.r[2];
-    h.steps_left = hit ? R.steps : 0;
+    // (a miss has spent its budget or escaped: 0; a progress-guard trip: -1)
+    h.steps_left = hit ? R.steps : min(R.steps, 0);
+    if (R.steps < 0 && P.guard_trips) atomicAdd(P.guard_trips, 1u);
     h.t = (float)R.tlast;  // (one rounding of the same double as before)
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
@@ -1360,8 +1371,9 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<false, true, true, SEG, 0, false, true>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr,
-                                                                    P.pos ? -1 : P.top_scene, P.top_scene);
+        const Hit h = trace<STATS, true, true, SEG, 0, false, true>(
+            P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+            &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
         if (P.pos) {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
@@ -1569,7 +1581,7 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
         else launch_dirs<AO, false>(dirs, grid, block, st, P);
         return;
     }
-    if (SHADE && !wide && dirs) {  // the sun's octant (shadow rays)
+    if (SHADE && !STATS && !wide && dirs) {  // the sun's octant (shadow rays)
         switch (dirs) {
             case 1: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); return;
             case 2: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); return;
@@ -1665,6 +1677,9 @@ static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& 
     }
 }
 
+// the tree's progress-guard trip counter: a u32 in its device side buffer (svo_internal.h kSideGuard)
+uint32_t* guard_word(const svo_tree* t) { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(t->d_pick) + kSideGuard); }
+
 int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, CastParams& P, int64_t& nthreads) {
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
@@ -1674,6 +1689,7 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     P.levels = t->levels;
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.top_solid = t->dev_top_y;  // the empty region above the tree's highest voxel row (trace: pre_top)
+    P.guard_trips = guard_word(t);
     set_ceilings(t, d, P, kCeilPrimary);
     P.steps = d->steps;
     P.flags = d->flags;
@@ -1747,6 +1763,7 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_ceilp) (void)hipFree(t->d_ceilp);
     t->d_ceil = t->d_ceilp = nullptr;
     t->ceil_levels = 0;
+    t->ceil_dev_n = 0;
     t->d_ao_plan = nullptr;
     t->ao_plan_steps = -1;
     (void)hipSetDevice(prev);
@@ -1762,33 +1779,97 @@ extern "C" void svo_tree_destroy(svo_tree* t) {
     delete t;
 }
 
-// the column ceilings of the host image (tree_ceilings), replacing the device copy
-static int upload_ceilings(svo_tree* t) {
-    std::vector<int16_t> c;
-    int64_t off[kCeilMax] = {0, 0, 0, 0};
-    const int32_t n = tree_ceilings(t, c, off);
-    if (t->d_ceil) (void)hipFree(t->d_ceil);
-    if (t->d_ceilp) (void)hipFree(t->d_ceilp);
-    t->d_ceil = t->d_ceilp = nullptr;
-    t->ceil_levels = 0;
-    if (n == 0) return SVO_OK;
-    // the pairs (level j, its parent block's level j+1; the last level paired with itself)
-    std::vector<uint32_t> pc(c.size());
+// The ceiling pairs of level j (its block's ceiling, low 16 bits; its level-(j+1) block's, high; the last level paired
+// with itself) over the blocks holding columns [x0, x1) x [z0, z1) — widened to whole parent blocks, whose change reaches
+// every child's pair.  Returns per level the first and last row written (level j's rows of blocks, row-major [z][x]).
+static void ceil_pairs(svo_tree* t, int32_t n, int64_t x0, int64_t z0, int64_t x1, int64_t z1, int64_t zr[kCeilMax][2]) {
     for (int32_t j = 0; j < n; j++) {
         const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
         const int32_t up = j + 1 < n ? j + 1 : j, sh = up > j ? 2 : 0;
+        const int32_t ush = 2 * (kCeilK0 + up), bsh = 2 * (kCeilK0 + j);
         const int64_t rows_up = rows >> sh;
-        for (int64_t z = 0; z < rows; z++)
-            for (int64_t x = 0; x < rows; x++)
-                pc[off[j] + z * rows + x] = (uint32_t)(uint16_t)c[off[j] + z * rows + x] |
-                                            ((uint32_t)(uint16_t)c[off[up] + (z >> sh) * rows_up + (x >> sh)] << 16);
+        const int64_t bz0 = (z0 >> ush) << (ush - bsh), bz1 = std::min(rows, (((z1 - 1) >> ush) + 1) << (ush - bsh));
+        const int64_t bx0 = (x0 >> ush) << (ush - bsh), bx1 = std::min(rows, (((x1 - 1) >> ush) + 1) << (ush - bsh));
+        const int16_t* c = t->ceil_host.data();
+        for (int64_t z = bz0; z < bz1; z++)
+            for (int64_t x = bx0; x < bx1; x++)
+                t->ceilp_host[t->ceil_off[j] + z * rows + x] = (uint32_t)(uint16_t)c[t->ceil_off[j] + z * rows + x] |
+                                                                 ((uint32_t)(uint16_t)c[t->ceil_off[up] + (z >> sh) * rows_up + (x >> sh)] << 16);
+        zr[j][0] = bz0;
+        zr[j][1] = bz1;
     }
-    HIP_TRY(hipMalloc(&t->d_ceil, c.size() * sizeof(int16_t)), SVO_ENOMEM);
-    HIP_TRY(hipMemcpy(t->d_ceil, c.data(), c.size() * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
-    HIP_TRY(hipMalloc(&t->d_ceilp, pc.size() * sizeof(uint32_t)), SVO_ENOMEM);
-    HIP_TRY(hipMemcpy(t->d_ceilp, pc.data(), pc.size() * sizeof(uint32_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+}
+
+// the column ceilings of the host image (tree_ceilings) and their pairs, replacing the device copies (the device
+// buffers are kept when their size is unchanged)
+static int upload_ceilings(svo_tree* t) {
+    int32_t n = 0;
+    int64_t zr[kCeilMax][2];
+    try {
+        int64_t off[kCeilMax] = {0, 0, 0, 0};
+        n = tree_ceilings(t, t->ceil_host, off);
+        for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = t->ceilp_off[j] = off[j];
+        t->ceilp_host.assign(t->ceil_host.size(), 0u);
+        if (n > 0) {
+            const int64_t e = (int64_t)1 << (2 * t->levels);
+            ceil_pairs(t, n, 0, 0, e, e, zr);
+        }
+    } catch (const std::bad_alloc&) {
+        t->ceil_host.clear();
+        t->ceilp_host.clear();
+        n = -1;
+    }
+    t->ceil_dirty.clear();
+    if (n <= 0 || (int64_t)t->ceil_host.size() != t->ceil_dev_n) {
+        if (t->d_ceil) (void)hipFree(t->d_ceil);
+        if (t->d_ceilp) (void)hipFree(t->d_ceilp);
+        t->d_ceil = t->d_ceilp = nullptr;
+        t->ceil_dev_n = 0;
+    }
+    t->ceil_levels = 0;
+    if (n < 0) SVO_FAIL(SVO_ENOMEM, "column ceilings: out of host memory");
+    if (n == 0) return SVO_OK;
+    const size_t m = t->ceil_host.size();
+    if (!t->d_ceil) {
+        HIP_TRY(hipMalloc(&t->d_ceil, m * sizeof(int16_t)), SVO_ENOMEM);
+        HIP_TRY(hipMalloc(&t->d_ceilp, m * sizeof(uint32_t)), SVO_ENOMEM);
+        t->ceil_dev_n = (int64_t)m;
+    }
+    HIP_TRY(hipMemcpy(t->d_ceil, t->ceil_host.data(), m * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    HIP_TRY(hipMemcpy(t->d_ceilp, t->ceilp_host.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     t->ceil_levels = n;
-    for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = t->ceilp_off[j] = off[j];
+    return SVO_OK;
+}
+
+// after edits: only the columns svo_tree_update touched are recomputed (tree walks restricted to them), and only the
+// rows of the tables that changed travel, into the device buffers already there
+static int sync_ceilings(svo_tree* t) {
+    if (t->ceil_dirty.empty()) return SVO_OK;
+    if (t->ceil_levels == 0 || !t->d_ceil) {
+        t->ceil_dirty.clear();
+        return SVO_OK;
+    }
+    const int32_t n = t->ceil_levels;
+    std::vector<std::array<int64_t, 4>> rects;
+    rects.swap(t->ceil_dirty);
+    for (const auto& r : rects) {
+        int64_t zr[kCeilMax][2];
+        try {
+            ceilings_update_rect(t, t->ceil_host, t->ceil_off, n, r[0], r[1], r[2], r[3]);
+            ceil_pairs(t, n, r[0], r[1], r[2], r[3], zr);
+        } catch (const std::bad_alloc&) {
+            SVO_FAIL(SVO_ENOMEM, "svo_tree_sync: column ceilings: out of host memory");
+        }
+        for (int32_t j = 0; j < n; j++) {
+            const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
+            const int64_t lo = t->ceil_off[j] + zr[j][0] * rows, cnt = (zr[j][1] - zr[j][0]) * rows;
+            if (cnt <= 0) continue;
+            HIP_TRY(hipMemcpy(reinterpret_cast<int16_t*>(t->d_ceil) + lo, t->ceil_host.data() + lo, cnt * sizeof(int16_t),
+                              hipMemcpyHostToDevice), SVO_EDEVICE);
+            HIP_TRY(hipMemcpy(reinterpret_cast<uint32_t*>(t->d_ceilp) + lo, t->ceilp_host.data() + lo, cnt * sizeof(uint32_t),
+                              hipMemcpyHostToDevice), SVO_EDEVICE);
+        }
+    }
     return SVO_OK;
 }
 
@@ -1821,7 +1902,7 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
     const uint64_t ncap = std::min<uint64_t>(t->nodes.size() + t->nodes.size() / 8 + 65536, 1ull << 32);
     const uint64_t mcap = std::min<uint64_t>(t->mats.size() + t->mats.size() / 8 + 65536, 1ull << 32);
     const size_t nb = ncap * sizeof(Node), mb = mcap * sizeof(uint16_t);
-    const size_t wb = 4096;
+    const size_t wb = kSideBytes;
     HIP_TRY(hipMalloc(&t->d_nodes, nb), SVO_ENOMEM);
     HIP_TRY(hipMalloc(&t->d_mats, mb), SVO_ENOMEM);
     HIP_TRY(hipMalloc(&t->d_pick, wb), SVO_ENOMEM);
@@ -1845,7 +1926,7 @@ extern "C" int svo_upload(svo_tree* t, int32_t device) {
 int svo::adopt_device(svo_tree* t, int32_t device, void* d_nodes, uint64_t node_cap, void* d_mats, uint64_t mat_cap) {
     tree_release_device(t);
     HIP_TRY(hipSetDevice(device), SVO_EDEVICE);
-    const size_t wb = 4096;
+    const size_t wb = kSideBytes;
     t->d_nodes = d_nodes;
     t->d_mats = d_mats;
     HIP_TRY(hipMalloc(&t->d_pick, wb), SVO_ENOMEM);
@@ -1870,6 +1951,9 @@ extern "C" int svo_tree_sync(svo_tree* t) {
     if (!t) SVO_FAIL(SVO_EINVAL, "svo_tree_sync: NULL tree");
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_sync: tree not uploaded (svo_upload)");
     if (t->full_upload || t->nodes.size() > t->dev_node_cap || t->mats.size() > t->dev_mat_cap) return svo_upload(t, t->device);
+    if (t->nodes.size() == t->synced_nodes && t->mats.size() == t->synced_mats && t->dirty_nodes.empty() && !t->palette_dirty &&
+        t->ceil_dirty.empty())
+        return SVO_OK;  // nothing changed since the last upload / sync
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     Node* dn = reinterpret_cast<Node*>(t->d_nodes);
     if (t->nodes.size() > t->synced_nodes)
@@ -1894,7 +1978,7 @@ extern "C" int svo_tree_sync(svo_tree* t) {
     t->synced_nodes = t->nodes.size();
     t->dev_top_y = tree_top_y(t);
     t->synced_mats = t->mats.size();
-    return upload_ceilings(t);
+    return sync_ceilings(t);
 }
 
 // ================================================================================================
@@ -1907,7 +1991,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: t must be a solid-view tree (the scene goes in svo_shade_desc.scene)");
     if (d->steps < 0 || sd->shadow_steps < 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: negative step budget");
     if (d->ao_samples != 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: AO is a separate pass (ao_samples must be 0)");
-    if (d->flags & (SVO_CAST_STATS | SVO_CAST_TIMELINE)) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: no diagnostics in the shading pass");
+    if (d->flags & SVO_CAST_TIMELINE) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: no block timeline in the shading pass (SVO_CAST_STATS only)");
+    if ((d->flags & SVO_CAST_STATS) && !d->stats) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: SVO_CAST_STATS without a stats buffer");
     if (o && (!o->pos_steps || !o->t || !o->info)) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: incomplete hit buffers");
     if (d->ray_dirs) {
         if (d->n_rays < 0) SVO_FAIL(SVO_EINVAL, "svo_shade_rays: negative ray count");
@@ -1945,8 +2030,9 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         if (P.sun[k] < 0.0f) sun_dirs += 1 << k;
         else if (!(P.sun[k] > 0.0f)) sun_dirs = 0;
     }
-    launch_cast<false, false, false, true>(wide_nodes(t, d->flags) || wide_nodes(sc, d->flags), true, dim3((uint32_t)blocks), dim3(kBlock),
-                                           (hipStream_t)stream, P, sun_dirs);
+    const bool wide = wide_nodes(t, d->flags) || wide_nodes(sc, d->flags);
+    if (P.flags & SVO_CAST_STATS) launch_cast<true, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
+    else launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, sun_dirs);
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return SVO_OK;
 }
@@ -2031,6 +2117,7 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     P.wmask = (1u << (2 * t->levels)) - 1u;
     P.mode = MODE_SINGLE;
     P.top_solid = t->dev_top_y;
+    P.guard_trips = guard_word(t);
     P.steps = steps;
     for (int a = 0; a < 3; a++) {
         P.org[a] = pos[a];
@@ -2055,6 +2142,30 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
         const Material& m = t->palette[(info & HIT_BIT) ? (info & MAT_MASK) : 0u];
         *block = svo_block{m.flags, m.color, m.meta};
     }
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32_t* pairs, int64_t cap, int32_t* levels, int64_t* n) {
+    if (!t || !levels || !n) SVO_FAIL(SVO_EINVAL, "svo_tree_device_ceilings: NULL argument");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_device_ceilings: tree not uploaded (svo_upload)");
+    *levels = t->ceil_levels;
+    *n = t->ceil_levels > 0 ? t->ceil_dev_n : 0;
+    if ((ceil || pairs) && cap < *n) SVO_FAIL(SVO_ERANGE, "svo_tree_device_ceilings: buffer too small");
+    if (*n == 0) return SVO_OK;
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    if (ceil) HIP_TRY(hipMemcpy(ceil, t->d_ceil, *n * sizeof(int16_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
+    if (pairs) HIP_TRY(hipMemcpy(pairs, t->d_ceilp, *n * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_guard_trips(const svo_tree* t, uint64_t* trips, int32_t reset) {
+    if (!t || !trips) SVO_FAIL(SVO_EINVAL, "svo_tree_guard_trips: NULL argument");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_guard_trips: tree not uploaded (svo_upload)");
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    uint32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, guard_word(t), sizeof(v), hipMemcpyDeviceToHost), SVO_EDEVICE);
+    if (reset) HIP_TRY(hipMemset(guard_word(t), 0, sizeof(v)), SVO_EDEVICE);
+    *trips = v;
     return SVO_OK;
 }
 

@@ -4,10 +4,12 @@
 
 #include <stdint.h>
 
+#include <array>
 #include <mutex>
 #include <string>
 #include <vector>
 
+#include "../../include/svo_rt.h"
 #include "svo_common.h"
 
 namespace svo {
@@ -51,7 +53,7 @@ struct svo_tree {
     int32_t device = -1;
     void* d_nodes = nullptr;
     void* d_mats = nullptr;
-    void* d_pick = nullptr;   // the pick ray's result record (svo_cast_ray_from_cam), 64 B
+    void* d_pick = nullptr;   // device side buffer (kSideBytes): the pick ray's record, the guard-trip counter (offsets below)
     void* d_pal = nullptr;    // palette for shading: u64 colour[n] then u32 flags[n]
     // hemisphere AO plan (svo_cast.hip, built on first use for (ao_samples, ao_steps))
     mutable void* d_ao_plan = nullptr;
@@ -80,16 +82,31 @@ struct svo_tree {
     // its level-(j+1) block (high 16 bits; the last level repeats its own), uint32 at element ceilp_off[j] of d_ceilp
     void* d_ceilp = nullptr;
     int64_t ceilp_off[4] = {0, 0, 0, 0};
+    int64_t ceil_dev_n = 0;            // elements of the d_ceil / d_ceilp allocations
+    std::vector<int16_t> ceil_host;    // the host copies of d_ceil / d_ceilp (svo_tree_sync updates them in place)
+    std::vector<uint32_t> ceilp_host;
+    // column rectangles {x0, z0, x1, z1} (wrapped, half-open) whose ceilings svo_tree_update's edits may have changed
+    std::vector<std::array<int64_t, 4>> ceil_dirty;
 };
 
 namespace svo {
+// the tree's device side buffer (svo_tree.d_pick): byte offsets
+constexpr size_t kSidePick = 0;     // svo_cast_ray_from_cam's result record (64 B)
+constexpr size_t kSideGuard = 256;  // u32: progress-guard trips of every launch over the tree (svo_tree_guard_trips)
+constexpr size_t kSideBytes = 4096;
 int32_t tree_top_y(const svo_tree* t);  // svo_world.cpp
 // Column ceilings (svo_world.cpp): per aligned block of 4^k x 4^k columns, k = kCeilK0 .. levels - 1 (at
 // most kCeilMax levels), the highest stored voxel row in those columns (-1: none) — every voxel above it
 // in the block is empty, whatever the tree holds (overhangs included).  Level j's blocks are row-major
 // [z][x] at out[off[j] ..]; returns the number of levels.
-constexpr int32_t kCeilK0 = 2, kCeilMax = 4;  // 16-, 64-, 256- and 1024-column blocks
+constexpr int32_t kCeilK0 = SVO_CEIL_K0, kCeilMax = 4;  // 16-, 64-, 256- and 1024-column blocks
 int32_t tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t off[kCeilMax]);
+// levels 1 .. nlev-1 re-derived over the blocks holding columns [x0, x1) x [z0, z1)
+void ceilings_coarsen(const svo_tree* t, std::vector<int16_t>& out, const int64_t off[kCeilMax], int32_t nlev, int64_t x0, int64_t z0,
+                      int64_t x1, int64_t z1);
+// every level over the columns [x0, x1) x [z0, z1) recomputed from the tree (an edit's region: svo_tree_sync)
+void ceilings_update_rect(const svo_tree* t, std::vector<int16_t>& out, const int64_t off[kCeilMax], int32_t nlev, int64_t x0, int64_t z0,
+                          int64_t x1, int64_t z1);
 void tree_release_device(svo_tree* t);  // svo_cast.hip
 // take over device arrays built on `device` (node_cap / mat_cap elements allocated, the host image
 // already equal to their first nodes.size() / mats.size() elements): svo_cast.hip

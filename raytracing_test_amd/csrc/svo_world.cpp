@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <system_error>
 #include <deque>
 #include <functional>
 #include <unordered_map>
@@ -604,6 +605,10 @@ extern "C" int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* x
         }
         // the child of A on the path, re-linearised from the world
         const uint32_t s = child_slot(x, y, z, (uint32_t)(2 * (L - 1 - da)));
+        {  // its columns: the only ones whose ceilings can change (svo_tree_sync)
+            const int64_t cs = (int64_t)1 << (2 * (L - 1 - da)), cx = (int64_t)(x & ~(uint32_t)(cs - 1)), cz = (int64_t)(z & ~(uint32_t)(cs - 1));
+            t->ceil_dirty.push_back({cx, cz, cx + cs, cz + cs});
+        }
         const WorldRegion r = world_region(w, em.solid, x, y, z, da + 1);
         Node rec{0, 0, K_INTERIOR};
         bool empty;
@@ -1077,32 +1082,98 @@ int32_t svo::tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t
         // the root's children by column (x, z slot): each thread walks the four children over one
         // quarter x quarter of the columns, so the blocks it writes are its own
         const int32_t cs = 1 << (2 * (t->levels - 1));
+        auto quadrant = [&, cs](uint32_t xz) {
+            CeilWalk w = cw;
+            for (uint32_t y = 0; y < 4; y++) {
+                const uint32_t sl = ((xz >> 2) << 4) | (y << 2) | (xz & 3u);
+                if (!((root.mask >> sl) & 1ull)) continue;
+                const uint32_t ci = root.ref + (uint32_t)__builtin_popcountll(root.mask & ((1ull << sl) - 1ull));
+                w.walk(ci, (int32_t)(xz & 3u) * cs, (int32_t)y * cs, (int32_t)(xz >> 2) * cs, 1);
+            }
+        };
         std::vector<std::thread> th;
-        for (uint32_t xz = 0; xz < 16; xz++)
-            th.emplace_back([&, xz] {
-                CeilWalk w = cw;
-                for (uint32_t y = 0; y < 4; y++) {
-                    const uint32_t sl = ((xz >> 2) << 4) | (y << 2) | (xz & 3u);
-                    if (!((root.mask >> sl) & 1ull)) continue;
-                    const uint32_t ci = root.ref + (uint32_t)__builtin_popcountll(root.mask & ((1ull << sl) - 1ull));
-                    w.walk(ci, (int32_t)(xz & 3u) * cs, (int32_t)y * cs, (int32_t)(xz >> 2) * cs, 1);
-                }
-            });
+        uint32_t started = 0;
+        try {
+            for (; started < 16; started++) th.emplace_back(quadrant, started);
+        } catch (const std::system_error&) {
+            // (no more threads: the quadrants not started are walked here)
+        }
+        for (uint32_t xz = started; xz < 16; xz++) quadrant(xz);
         for (auto& x : th) x.join();
     }
-    for (int32_t j = 1; j < nlev; j++) {  // 4 x 4 maxima of the finer level
+    ceilings_coarsen(t, out, off, nlev, 0, 0, (int64_t)1 << (2 * t->levels), (int64_t)1 << (2 * t->levels));
+    return nlev;
+}
+
+// levels 1 .. nlev-1 as 4 x 4 maxima of the finer level, over the blocks that hold columns [x0, x1) x [z0, z1)
+void svo::ceilings_coarsen(const svo_tree* t, std::vector<int16_t>& out, const int64_t off[kCeilMax], int32_t nlev, int64_t x0, int64_t z0,
+                           int64_t x1, int64_t z1) {
+    for (int32_t j = 1; j < nlev; j++) {
+        const int32_t bsh = 2 * (kCeilK0 + j);
         const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j)), fine = rows * 4;
         const int16_t* f = out.data() + off[j - 1];
         int16_t* c = out.data() + off[j];
-        for (int64_t bz = 0; bz < rows; bz++)
-            for (int64_t bx = 0; bx < rows; bx++) {
+        for (int64_t bz = z0 >> bsh; bz < std::min(rows, ((z1 - 1) >> bsh) + 1); bz++)
+            for (int64_t bx = x0 >> bsh; bx < std::min(rows, ((x1 - 1) >> bsh) + 1); bx++) {
                 int16_t v = -1;
                 for (int64_t dz = 0; dz < 4; dz++)
                     for (int64_t dx = 0; dx < 4; dx++) v = std::max(v, f[(bz * 4 + dz) * fine + bx * 4 + dx]);
                 c[bz * rows + bx] = v;
             }
     }
-    return nlev;
+}
+
+// The finest level over the columns [x0, x1) x [z0, z1) (aligned to the finest blocks) recomputed from the tree: the
+// blocks are cleared, then a walk that enters only the nodes whose columns meet the rectangle raises them again.
+namespace {
+struct CeilRectWalk {
+    CeilWalk cw;
+    int64_t x0, z0, x1, z1;
+    void walk(uint32_t ni, int64_t nx, int32_t ny, int64_t nz, int depth) {
+        const svo_tree* t = cw.t;
+        const Node& n = t->nodes[ni];
+        const int64_t size = (int64_t)1 << (2 * (t->levels - depth));
+        const uint32_t kind = node_kind(n.info);
+        if (kind == K_SOLID) {
+            const int32_t bsh = cw.bsh;
+            const int64_t ax = std::max(nx, x0), bx = std::min(nx + size, x1), az = std::max(nz, z0), bz = std::min(nz + size, z1);
+            for (int64_t z = az >> bsh; z <= (bz - 1) >> bsh; z++)
+                for (int64_t x = ax >> bsh; x <= (bx - 1) >> bsh; x++) cw.put(x, z, ny + (int32_t)size - 1);
+            return;
+        }
+        if (kind == K_BRICK) {
+            cw.walk(ni, (int32_t)nx, ny, (int32_t)nz, depth);
+            return;
+        }
+        const int64_t cs = size >> 2;
+        uint64_t m = n.mask;
+        uint32_t ci = n.ref;
+        while (m) {
+            const uint32_t sl = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const int64_t cx = nx + (int64_t)(sl & 3u) * cs, cz = nz + (int64_t)(sl >> 4) * cs;
+            const uint32_t c = ci++;
+            if (cx >= x1 || cx + cs <= x0 || cz >= z1 || cz + cs <= z0) continue;
+            walk(c, cx, ny + (int32_t)((sl >> 2) & 3u) * (int32_t)cs, cz, depth + 1);
+        }
+    }
+};
+}  // namespace
+
+void svo::ceilings_update_rect(const svo_tree* t, std::vector<int16_t>& out, const int64_t off[kCeilMax], int32_t nlev, int64_t x0,
+                               int64_t z0, int64_t x1, int64_t z1) {
+    if (nlev <= 0 || t->nodes.empty()) return;
+    const int32_t bsh = 2 * kCeilK0;
+    const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0));
+    x0 = (x0 >> bsh) << bsh;
+    z0 = (z0 >> bsh) << bsh;
+    x1 = (((x1 - 1) >> bsh) + 1) << bsh;
+    z1 = (((z1 - 1) >> bsh) + 1) << bsh;
+    for (int64_t bz = z0 >> bsh; bz < z1 >> bsh; bz++)
+        for (int64_t bx = x0 >> bsh; bx < x1 >> bsh; bx++) out[off[0] + bz * rows + bx] = -1;
+    CeilRectWalk w{CeilWalk{t, bsh, rows, out.data() + off[0]}, x0, z0, x1, z1};
+    w.walk(0, 0, 0, 0, 0);
+    ceilings_coarsen(t, out, off, nlev, x0, z0, x1, z1);
 }
 
 extern "C" int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n) {

@@ -107,3 +107,56 @@ def test_patched_tree_casts_match_oracle(rt, oracle_mod, torch_cuda):
     a = tree.shade_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 240, 136, 300, sun=rt.sun_dir())
     b = fresh.shade_frame((4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0)), 240, 136, 300, sun=rt.sun_dir())
     assert torch_cuda.equal(a, b)
+
+
+def _pairs_of(c, E, k0, lv):
+    """the pair table the kernels read, derived from the ceilings (svo_cast.hip ceil_pairs)"""
+    offs, o = [], 0
+    for j in range(lv):
+        rows = E >> (2 * (k0 + j))
+        offs.append((o, rows))
+        o += rows * rows
+    p = np.zeros(len(c), np.uint32)
+    for j in range(lv):
+        o, rows = offs[j]
+        up = j + 1 if j + 1 < lv else j
+        ou, ru = offs[up]
+        sh = 2 if up > j else 0
+        lvl = c[o:o + rows * rows].reshape(rows, rows).astype(np.uint16).astype(np.uint32)
+        par = c[ou:ou + ru * ru].reshape(ru, ru).astype(np.uint16).astype(np.uint32)
+        p[o:o + rows * rows] = (lvl | (np.repeat(np.repeat(par, 1 << sh, 0), 1 << sh, 1) << 16)).reshape(-1)
+    return p
+
+
+def test_sync_updates_device_ceilings_incrementally(rt, torch_cuda):
+    """svo_tree_sync recomputes only the edited columns' ceilings and uploads their rows into the
+    device tables already there.  After every edit + sync the tables in HBM equal a full recomputation over
+    the patched tree (svo_tree_ceilings) and the pairs derived from it; a sync with nothing changed is a no-op."""
+    import time
+
+    rng = np.random.default_rng(5)
+    w = rt.World.reference()
+    tree = w.build().upload(0)
+    E = 1 << (2 * w.levels)
+    lv0, c0, p0 = tree.device_ceilings()
+    assert lv0 >= 2
+    times = []
+    for step in range(6):
+        if step % 2 == 0:  # raise columns (a tower), then carve terrain away
+            pts = np.stack([rng.integers(0, 400, 30), rng.integers(60, 200, 30), rng.integers(0, 400, 30)], 1)
+            w.put_blocks(pts, np.zeros(len(pts), np.uint32), np.full(len(pts), 77, np.uint64))
+        else:
+            pts = np.stack([rng.integers(0, 200, 60), rng.integers(1, 64, 60), rng.integers(0, 200, 60)], 1)
+            for p in pts:
+                w.delete_block(*[int(v) for v in p])
+        t0 = time.perf_counter()
+        tree.update(w, pts)
+        tree.sync()
+        times.append(time.perf_counter() - t0)
+        lv, c, p = tree.device_ceilings()
+        full = np.concatenate([x.reshape(-1) for x in tree.ceilings()])
+        assert lv == lv0 and np.array_equal(c, full), "step %d: device ceilings differ from a full recomputation" % step
+        assert np.array_equal(p, _pairs_of(full, E, rt.CEIL_K0, lv)), "step %d: pair table" % step
+    tree.sync()  # nothing changed: no-op
+    assert np.array_equal(tree.device_ceilings()[1], c)
+    print("edit + sync of 30-60 blocks: %s ms" % ", ".join("%.2f" % (x * 1e3) for x in times))

@@ -424,6 +424,9 @@ def test_depth12_full_frame_parity(rt, depth12, oracle12):
     assert ref["rc"] == 0
     compare(rt, depth12, out, ref, "C3 full frame")
     assert (ref["hit"] != 0).mean() > 0.99  # every ray points down and lands on terrain
+    # no launch over the tree so far ended a ray on the progress guard (such a ray would carry stepsLeft -1)
+    assert depth12.guard_trips() == 0
+    assert (rt.decode_hits(out)["steps"] >= 0).all()
 
 
 @pytest.mark.parametrize("org", [(4.5, 90.5, 4.5), (-3.5, 80.5, -2.5), (2000.5, 70.0, 1000.5)])
