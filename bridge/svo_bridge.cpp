@@ -14,6 +14,7 @@ svo_world* g_world = nullptr;
 svo_tree* g_tree = nullptr;   // solid view: castRayFromCam, primary frames, shadow rays
 svo_tree* g_scene = nullptr;  // full view (water stored): what the shaded frame's rays walk (low_res.frag)
 bool g_rebuild = true;  // the world changed without a tree to patch (genWorld, edits before the first upload)
+svo_ray_result* g_look = nullptr;  // device record of the frame's lookingAtBlock pick ray (svoRenderShaded)
 
 void check(int rc, const char* what) {
     if (rc) {
@@ -116,6 +117,7 @@ void updateSsboData() {
 }
 
 svo_tree* svoTree() { return g_tree; }
+svo_tree* svoScene() { return g_scene; }
 
 namespace RAY_CASTER {
 // ray_caster.cpp:54-87 on the GPU (one ray, synchronous)
@@ -151,15 +153,17 @@ void svoCastPrimaryRays(int32_t width, int32_t height, int32_t steps, int32_t* p
 void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream, float time) {
     if (!g_tree) updateSsboData();
     const svo_cast_desc d = frame_desc(width, height, 300);  // low_res.frag:310
-    const RayResult look = RAY_CASTER::castRayFromCam(30);    // main.cpp:81, the lookingAtBlock uniform (:89)
+    // main.cpp:81, castRayFromCam(30) for the lookingAtBlock uniform (:89), cast on the frame's stream into a
+    // device record the shading kernel reads: the frame loop never waits for the host
+    if (!g_look) check(hipMalloc(reinterpret_cast<void**>(&g_look), 256) == hipSuccess ? 0 : SVO_ENOMEM, "hipMalloc (look-at record)");
+    float o[3], dir[3];
+    camera(o, dir);
+    check(svo_cast_ray_from_cam_async(g_tree, o, dir, 30, g_look, stream), "svo_cast_ray_from_cam_async");
     svo_shade_desc sd{};
     sd.sun_dir[0] = sun.x;
     sd.sun_dir[1] = sun.y;
     sd.sun_dir[2] = sun.z;
-    sd.look_at[0] = look.pos.x;
-    sd.look_at[1] = look.pos.y;
-    sd.look_at[2] = look.pos.z;
-    sd.look_at_valid = 1;
+    sd.look_at_dev = g_look;
     sd.shadow_steps = 75;  // low_res.frag:382
     sd.scene = g_scene;    // water refracts and tints (low_res.frag:214-229)
     sd.time = time;        // the deltaTime uniform

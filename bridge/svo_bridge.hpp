@@ -24,7 +24,10 @@ void updateSsboData();
 // device buffers (24 B per pixel, include/svo_rt.h svo_hits), asynchronously on `stream`
 void svoCastPrimaryRays(int32_t width, int32_t height, int32_t steps, int32_t* pos_steps, float* t, uint32_t* info, hipStream_t stream);
 // the same frame shaded (low_res.frag's colour model, svo_shade_rays, water refracting through the
-// full-view scene the shim keeps beside the solid tree): one float4 per pixel; time = deltaTime
+// full-view scene the shim keeps beside the solid tree): one float4 per pixel; time = deltaTime.  The
+// lookingAtBlock pick ray runs on `stream` too (svo_cast_ray_from_cam_async): no host round trip per frame
 void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t stream, float time = 0.0f);
 // the tree the shim keeps in HBM (for direct use of the C ABI, e.g. svo_exchange_frames)
 svo_tree* svoTree();
+// the full-view scene tree svoRenderShaded's rays walk
+svo_tree* svoScene();

@@ -284,6 +284,11 @@ int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir
    only a wrong crossing count can cause it).  Such a ray's record has stepsLeft = -1 and no hit; the count
    should be 0.  reset != 0 zeroes the counter.  Synchronous (reads device memory). */
 int svo_tree_guard_trips(const svo_tree* t, uint64_t* trips, int32_t reset);
+/* the same pick ray, stream-ordered and without a host round trip: the result (svo_ray_result, 28 B) is
+   written to d_result, device memory aligned to 16 bytes, on hip_stream (two small launches) — for the
+   per-frame lookingAtBlock ray (main.cpp:81,89; svo_shade_desc.look_at_dev).  The block is not returned. */
+int svo_cast_ray_from_cam_async(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* d_result,
+                                void* hip_stream);
 int svo_sync(void* hip_stream);
 
 /* Wire formats of hit records for the exchange between GPUs (the tile-row gather):
@@ -371,6 +376,9 @@ typedef struct {
     const svo_tree* scene; /* SVO_VIEW_ALL tree the primary / reflected / refracted ray walks (NULL: t);
                               shadow rays walk t (liquid passes) */
     float time;            /* deltaTime uniform of the liquid wobble (low_res.frag:226) */
+    const svo_ray_result* look_at_dev; /* device record (NULL: use look_at / look_at_valid): lookingAtBlock is its
+                              pos, read by the kernel — e.g. written by svo_cast_ray_from_cam_async on the same
+                              stream, so a frame needs no host round trip (main.cpp:81,89) */
 } svo_shade_desc;
 
 /* asynchronous on hip_stream; rgba: device float4 per ray; hits: optional hit records (may be NULL) */

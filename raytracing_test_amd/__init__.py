@@ -119,7 +119,7 @@ class Hits(C.Structure):
 
 class ShadeDesc(C.Structure):
     _fields_ = [("sun_dir", C.c_float * 3), ("look_at", C.c_int32 * 3), ("look_at_valid", C.c_int32), ("shadow_steps", C.c_int32),
-                ("scene", C.c_void_p), ("time", C.c_float)]
+                ("scene", C.c_void_p), ("time", C.c_float), ("look_at_dev", C.c_void_p)]
 
 
 # globals.cpp:23: sun = normalize(vec3(2, 1, 4))
@@ -141,7 +141,7 @@ ABI_SYMBOLS = (
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
-    "svo_tree_guard_trips", "svo_tree_device_ceilings",
+    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_cast_ray_from_cam_async",
 )
 
 
@@ -183,7 +183,8 @@ def lib():
                      ("svo_exchange_wire", [vp, vp, C.POINTER(CastDesc), vp, vp, C.POINTER(Hits), vp]),
                      ("svo_tree_ceilings", [vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
                      ("svo_tree_guard_trips", [vp, C.POINTER(C.c_uint64), i32]),
-                     ("svo_tree_device_ceilings", [vp, vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)])):
+                     ("svo_tree_device_ceilings", [vp, vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
+                     ("svo_cast_ray_from_cam_async", [vp, f3, f3, i32, vp, vp])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
     L.svo_build_terrain.argtypes = [i32, i32, i32, i32, C.POINTER(vp)]
@@ -695,12 +696,16 @@ class Tree:
 
     def shade(self, desc, rgba, sun=None, look_at=None, shadow_steps=75, out=None, stream=None, scene=None, time=0.0):
         """Launch the shading pass (svo_shade_rays) for `desc`: rgba is a (n, 4) float32 device tensor.
-        scene: a VIEW_ALL Tree of the same world (liquid refracts and tints); time: the wobble's deltaTime."""
+        scene: a VIEW_ALL Tree of the same world (liquid refracts and tints); time: the wobble's deltaTime.
+        look_at: a voxel (x, y, z), or a device int32 tensor holding a svo_ray_result (cast_ray_from_cam_async
+        on the same stream) whose pos the kernel reads."""
         sd = ShadeDesc()
         sd.scene = scene._h if scene is not None else None
         sd.time = time
         sd.sun_dir[:] = [float(x) for x in (sun if sun is not None else sun_dir())]
-        if look_at is not None:
+        if look_at is not None and hasattr(look_at, "data_ptr"):
+            sd.look_at_dev = look_at.data_ptr()
+        elif look_at is not None:
             sd.look_at[:] = [int(x) for x in look_at]
             sd.look_at_valid = 1
         sd.shadow_steps = shadow_steps
@@ -724,6 +729,13 @@ class Tree:
         if sync:
             _check(lib().svo_sync(C.c_void_p(getattr(stream, "cuda_stream", stream)) if stream else None), "svo_sync")
         return (rgba, out) if with_hits else rgba
+
+    def cast_ray_from_cam_async(self, pos, cam_dir, steps, out, stream=None):
+        """svo_cast_ray_from_cam_async: the pick ray's RayResult (pos, last_pos, steps) written to `out` (an int32 device
+        tensor of >= 7 elements, 16-byte aligned) on `stream`, without a host round trip."""
+        s = getattr(stream, "cuda_stream", stream)
+        _check(lib().svo_cast_ray_from_cam_async(self._h, _f3(pos), _f3(cam_dir), steps, C.c_void_p(out.data_ptr()),
+                                                 C.c_void_p(s) if s else None), "svo_cast_ray_from_cam_async")
 
     def cast_ray_from_cam(self, pos, cam_dir, steps):
         """RAY_CASTER::castRayFromCam(steps) with the camera passed in: (RayResult, Block)."""

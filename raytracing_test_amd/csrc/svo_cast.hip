@@ -81,6 +81,7 @@ struct CastParams {
     float sun[3];
     int32_t look[3];
     int32_t look_valid, shadow_steps;
+    const int32_t* look_dev;    // device lookingAtBlock record (svo_ray_result: pos first) or null
     float time;                 // deltaTime of the liquid wobble (low_res.frag:226)
     const Node* snodes;         // shading: the solid-view tree the shadow rays walk (nodes: the scene)
     const uint16_t* smats;
@@ -1382,7 +1383,15 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
         const bool hit = (h.info & HIT_BIT) != 0u;
         const float* m = bn.m;  // finalColorMod
         float3 c;
-        if (P.look_valid && h.x == P.look[0] && h.y == P.look[1] && h.z == P.look[2]) {
+        int32_t lk[3] = {P.look[0], P.look[1], P.look[2]};
+        bool lv = P.look_valid != 0;
+        if (P.look_dev) {  // (uniform: the pick ray's record, written on this stream before the launch)
+            lk[0] = P.look_dev[0];
+            lk[1] = P.look_dev[1];
+            lk[2] = P.look_dev[2];
+            lv = true;
+        }
+        if (lv && h.x == lk[0] && h.y == lk[1] && h.z == lk[2]) {
             const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
             c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
         } else if (!hit) {
@@ -2019,6 +2028,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         P.look[k] = sd->look_at[k];
     }
     P.look_valid = sd->look_at_valid != 0;
+    P.look_dev = reinterpret_cast<const int32_t*>(sd->look_at_dev);
     P.shadow_steps = sd->shadow_steps;
     if (n == 0) return SVO_OK;
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
@@ -2097,18 +2107,13 @@ static int cast_launch(const svo_tree* t, const svo_cast_desc* d, const svo_hits
     return SVO_OK;
 }
 
-extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* out,
-                                     svo_block* block) {
-    if (!t || !pos || !dir || !out) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: NULL argument");
-    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_cast_ray_from_cam: tree not uploaded (svo_upload)");
-    if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: castRayFromCam semantics need a solid-view tree");
-    if (steps < 0) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: negative step budget");
+namespace {
+// one pick ray's hit record (int4 pos + steps, f32 t, u32 info at +0 / +16 / +20 of buf) on `stream`
+int pick_launch(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, void* buf, hipStream_t stream, const char* fn) {
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, std::string(fn) + ": tree not uploaded (svo_upload)");
+    if (t->view != SVO_VIEW_SOLID) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": castRayFromCam semantics need a solid-view tree");
+    if (steps < 0) SVO_FAIL(SVO_EINVAL, std::string(fn) + ": negative step budget");
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
-    void* buf = nullptr;
-    // the tree's own 64-B result record: no allocation per pick (the reference casts one every frame,
-    // main.cpp:81); one pick at a time per tree
-    std::lock_guard<std::mutex> lock(t->pick_mu);
-    buf = t->d_pick;
     CastParams P;
     memset(&P, 0, sizeof(P));
     P.nodes = reinterpret_cast<const Node*>(t->d_nodes);
@@ -2125,15 +2130,57 @@ extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], cons
     }
     P.pos = reinterpret_cast<int32_t*>(buf);
     P.t = reinterpret_cast<float*>(reinterpret_cast<char*>(buf) + 16);
-    P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 32);
-    launch_cast<false, false, false, false>(wide_nodes(t, 0), need_seg(P), dim3(1), dim3(kBlock), nullptr, P);
-    unsigned char host[64];
-    hipError_t e = hipMemcpy(host, buf, 64, hipMemcpyDeviceToHost);
+    P.info = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(buf) + 20);
+    launch_cast<false, false, false, false>(wide_nodes(t, 0), need_seg(P), dim3(1), dim3(kBlock), stream, P);
+    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+// the hit record at r (pick_launch) rewritten in place as a RayResult {pos, lastPos, steps} (ray_caster.hpp:6-10)
+__global__ __launch_bounds__(64) void k_pick_result(int32_t* r) {
+    if (threadIdx.x != 0) return;
+    const int32_t x = r[0], y = r[1], z = r[2], st = r[3];
+    const uint32_t info = (uint32_t)r[5];
+    int32_t last[3] = {x, y, z};
+    const uint32_t axis = (info >> AXIS_SHIFT) & 3u;
+    if (axis < 3u) last[axis] -= (info & NEG_BIT) ? -1 : 1;
+    r[0] = x;
+    r[1] = y;
+    r[2] = z;
+    r[3] = last[0];
+    r[4] = last[1];
+    r[5] = last[2];
+    r[6] = st;
+}
+}  // namespace
+
+extern "C" int svo_cast_ray_from_cam_async(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* d_result,
+                                           void* stream) {
+    if (!t || !pos || !dir || !d_result) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam_async: NULL argument");
+    if (reinterpret_cast<uintptr_t>(d_result) & 15u) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam_async: d_result not 16-byte aligned");
+    int rc = pick_launch(t, pos, dir, steps, d_result, (hipStream_t)stream, "svo_cast_ray_from_cam_async");
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pick_result, dim3(1), dim3(64), 0, (hipStream_t)stream, reinterpret_cast<int32_t*>(d_result));
+    HIP_TRY(hipGetLastError(), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+extern "C" int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir[3], int32_t steps, svo_ray_result* out,
+                                     svo_block* block) {
+    if (!t || !pos || !dir || !out) SVO_FAIL(SVO_EINVAL, "svo_cast_ray_from_cam: NULL argument");
+    // the tree's own result record: no allocation per pick (the reference casts one every frame, main.cpp:81);
+    // one synchronous pick at a time per tree
+    std::lock_guard<std::mutex> lock(t->pick_mu);
+    void* buf = reinterpret_cast<char*>(t->d_pick) + kSidePick;
+    int rc = pick_launch(t, pos, dir, steps, buf, nullptr, "svo_cast_ray_from_cam");
+    if (rc) return rc;
+    unsigned char host[32];
+    hipError_t e = hipMemcpy(host, buf, 32, hipMemcpyDeviceToHost);
     if (e != hipSuccess) SVO_FAIL(SVO_EDEVICE, std::string("svo_cast_ray_from_cam: ") + hipGetErrorString(e));
     int32_t p4[4];
     uint32_t info;
     memcpy(p4, host, 16);
-    memcpy(&info, host + 32, 4);
+    memcpy(&info, host + 20, 4);
     for (int a = 0; a < 3; a++) out->pos[a] = out->last_pos[a] = p4[a];
     out->steps = p4[3];
     const uint32_t axis = (info >> AXIS_SHIFT) & 3u;

@@ -106,6 +106,41 @@ int main(int argc, char** argv) {
     int finite = 1;
     for (float v : img) finite &= isfinite(v) ? 1 : 0;
     fprintf(g_out, "\"shade_finite\": %d,\n", finite);
+    // the same frame with the pick ray cast on the host side (svo_cast_ray_from_cam, then look_at): the
+    // device look-at record must give the identical image
+    {
+        const RayResult look = RAY_CASTER::castRayFromCam(30);
+        svo_cast_desc d{};
+        d.origin[0] = cameraPos.x;
+        d.origin[1] = cameraPos.y;
+        d.origin[2] = cameraPos.z;
+        d.cam_dir[0] = cameraDir.x;
+        d.cam_dir[1] = cameraDir.y;
+        d.cam_dir[2] = cameraDir.z;
+        d.width = W;
+        d.height = H;
+        d.tile_row_step = 1;
+        d.steps = 300;
+        SVOCHK(svo_proj_plane(W, H, &d.ppx, &d.ppy));
+        svo_shade_desc sd{};
+        sd.sun_dir[0] = sun.x;
+        sd.sun_dir[1] = sun.y;
+        sd.sun_dir[2] = sun.z;
+        sd.look_at[0] = look.pos.x;
+        sd.look_at[1] = look.pos.y;
+        sd.look_at[2] = look.pos.z;
+        sd.look_at_valid = 1;
+        sd.shadow_steps = 75;
+        sd.scene = svoScene();
+        float* rgba2;
+        HIPCHK(hipMalloc(&rgba2, (size_t)N * 16));
+        SVOCHK(svo_shade_rays(svoTree(), &d, &sd, rgba2, nullptr, nullptr));
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<float> img2((size_t)N * 4);
+        HIPCHK(hipMemcpy(img2.data(), rgba2, (size_t)N * 16, hipMemcpyDeviceToHost));
+        fprintf(g_out, "\"shade_dev_look_eq_host\": %d,\n", memcmp(img.data(), img2.data(), img.size() * 4) == 0 ? 1 : 0);
+        HIPCHK(hipFree(rgba2));
+    }
     // single-rank exchange of a two-frame cast (frames 0 and 1 both displayed by rank 0)
     uint8_t uid[SVO_NCCL_UNIQUE_ID_BYTES];
     SVOCHK(svo_nccl_unique_id(uid));

@@ -67,6 +67,7 @@ def test_bridge_sequence_vs_oracle(rt, oracle_mod, bridge_out):
     fr = np.array(bridge_out["frame"], np.int64).reshape(-1, 4)
     assert np.array_equal(fr[:, :3], ref["pos"]) and np.array_equal(fr[:, 3], ref["steps"])
     assert bridge_out["shade_finite"] == 1
+    assert bridge_out["shade_dev_look_eq_host"] == 1  # the device look-at record (no host round trip) = the host pick
 
 
 def test_bridge_single_rank_exchange(bridge_out):

@@ -82,6 +82,40 @@ def test_shade_look_at_and_budget(rt, gtree, ref_world_oracle):
         _check(rgba, ref, rt.decode_hits(hits)["hit"], "look S=%d shadow=%d" % (S, shadow))
 
 
+def test_pick_ray_on_device(rt, gtree, torch_cuda):
+    """the per-frame pick ray (main.cpp:81,89) without a host round trip —
+    svo_cast_ray_from_cam_async writes the RayResult to device memory on the frame's stream, equal to the
+    synchronous svo_cast_ray_from_cam (hits, misses, a hit on the last step, budget 0), and the shading pass reads
+    lookingAtBlock from that record: the image equals the one with the host-side look_at, and the highlight shows."""
+    torch = torch_cuda
+    s = torch.cuda.Stream()
+    rec = torch.zeros(64, dtype=torch.int32, device="cuda")
+    for org, cd in CAMERAS + [((35.0, 50.0, 35.0), (0.0, -1.0, 0.0)), ((-20.5, 300.0, 7.25), (0.2, 1.0, 0.1))]:
+        cam_dir = rt.normalize(cd)
+        for steps in (0, 1, 7, 30, 300):
+            (pos, last, left), _ = gtree.cast_ray_from_cam(org, cam_dir, steps)
+            rec.fill_(-7)
+            gtree.cast_ray_from_cam_async(org, cam_dir, steps, rec, stream=s)
+            s.synchronize()
+            r = rec[:7].cpu().numpy()
+            assert tuple(r[:3]) == tuple(pos) and tuple(r[3:6]) == tuple(last) and r[6] == left, (org, cd, steps, r, pos, last, left)
+    org, cd = CAMERAS[0]
+    cam_dir = rt.normalize(cd)
+    (pos, _, _), _ = gtree.cast_ray_from_cam(org, cam_dir, 30)
+    d = gtree.frame_desc(org, cam_dir, 160, 90, 300)
+    a = torch.empty((160 * 90, 4), dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    none = torch.empty_like(a)
+    with torch.cuda.stream(s):
+        gtree.cast_ray_from_cam_async(org, cam_dir, 30, rec, stream=s)
+        gtree.shade(d, a, sun=rt.sun_dir(), look_at=rec, stream=s)
+        gtree.shade(d, b, sun=rt.sun_dir(), look_at=pos, stream=s)
+        gtree.shade(d, none, sun=rt.sun_dir(), stream=s)
+    s.synchronize()
+    assert torch.equal(a, b)
+    assert not torch.equal(a, none)  # the looked-at voxel is in view and highlighted
+
+
 def test_shade_other_suns(rt, gtree, ref_world_oracle):
     org, cd = CAMERAS[1]
     cam_dir = rt.normalize(cd)
