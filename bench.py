@@ -249,7 +249,16 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
     key = cfg["bray"]
     b = bray.get(key)
     model, bytes_model, extra = None, None, {}
-    if not args.shade and b is not None:  # (the shading pass has no §8(d) model)
+    sb = bray.get(key + "_shade") if args.shade else None
+    if sb is not None:
+        # the shading pass: §8(d)'s entries along every lookup its rays make (primary + reflections / refractions, and the
+        # shadow ray), oracle/bray.py c3_shade_entry
+        model = sb["bytes_per_ray"]
+        bytes_model = ("SURVEY.md §8d for the shading pass: B = 16 (E + R) + 4 E + 16 B rgba, E = %.2f node entries per pixel "
+                       "along the reference DDA paths of the primary ray with its reflections / refractions and of the 75-step shadow "
+                       "ray (restart model, liquid mode), R = %.3f root reads per pixel (%s_shade, profiles/bray.json)"
+                       % (sb["e_per_ray"], 1.0 + sb["shadow_rays_per_ray"], key))
+    if not args.shade and b is not None:
         model = b["bytes_per_ray"]
         if "e_child_per_ray" in b:
             bytes_model = ("SURVEY.md §8d B_ray = 16 (E_child + 1) + 4 E_child + 24 B hit record, E_child = %.2f node entries per ray "

@@ -2,8 +2,8 @@
 B_ray = 16*E_node + 4*E_child + B_out with E_node = E_child + 1, where E_child counts node entries
 along the reference DDA path under the shader's common-ancestor restart (low_res.frag:493-531) on
 the reference-format tree.  Writes profiles/bray.json, which bench.py reads (it never imports the
-oracle for this).  Usage: python oracle/bray.py [C3f]  (C3f: only the non-integral-camera C3 entry,
-merged into the existing file)
+oracle for this).  Usage: python oracle/bray.py [C3f | C2d8 | C3_shade]  (one entry only, merged into the existing file;
+C3_shade: the shading pass, see c3_shade_entry)
 """
 import json
 import os
@@ -36,7 +36,33 @@ def c2d8_entry():
             "tree": "depth-8 (4 levels, 256^3): clean root + genWorld putBlocks over 200 x 200 columns; C3 pose, S = 300"}
 
 
+SUN = (2.0, 1.0, 4.0)  # the reference sun (globals.cpp:23), normalised as rt.sun_dir() does
+
+
+def c3_shade_entry():
+    """bench.py --shade: the shading pass over the C3 frame with water (liquid mode), S = 16384, 75-step shadow rays.
+    B_ray = 16 (E + R) + 4 E + 16: E node entries per pixel under the restart model (primary with its reflections /
+    refractions, plus the shadow ray continuing from the primary's lookup state), R root reads per pixel (the primary
+    and, where one is cast, the shadow ray), and the 16-B rgba pixel (the bench writes no hit records)."""
+    t = O.Tree.terrain(6, 4096, 4096)
+    n = 1920 * 1080
+    e, sh, lk = t.shade_entries((4, 90, 4), O.normalize((1, -0.45, 1)), 1920, 1080, 16384, O.normalize(SUN), 75, nthreads=8,
+                                liquid=True)
+    E, R = e / n, 1.0 + sh / n
+    return {"e_per_ray": E, "shadow_rays_per_ray": sh / n, "lookups_per_ray": lk / n, "bytes_per_ray": 16 * (E + R) + 4 * E + 16,
+            "formula": "16 (E + R) + 4 E + 16 B rgba, R = 1 + shadow rays per pixel",
+            "tree": "depth-12 terrain (4096^2 columns), reference node/array format, liquid mode (water refracts); C3 pose, S = 16384, "
+                    "sun normalize(2,1,4), 75-step shadow rays"}
+
+
 def main():
+    if sys.argv[1:] == ["C3_shade"]:
+        path = os.path.join(ROOT, "profiles", "bray.json")
+        res = json.load(open(path))
+        res["C3_shade"] = c3_shade_entry()
+        json.dump(res, open(path, "w"), indent=1)
+        print(json.dumps(res["C3_shade"], indent=1))
+        return
     if sys.argv[1:] == ["C2d8"]:
         path = os.path.join(ROOT, "profiles", "bray.json")
         res = json.load(open(path))
@@ -64,6 +90,7 @@ def main():
                  "tree": "depth-12 terrain, reference node/array format with uniform regions collapsed"}
     res["C3f"] = c3f_entry()
     res["C2d8"] = c2d8_entry()
+    res["C3_shade"] = c3_shade_entry()
     # C4: §8(d) "for AO: add <= 5 steps x E per sample" -- the AO rays' node entries (each continues the
     # restart model from the primary's final lookup), 16 + 4 B per entry, per primary ray of the frame;
     # B_OUT grows by the 1-B AO count

@@ -1502,8 +1502,9 @@ static void o_sky(const float d[3], const float sun[3], float o[3]) {
 }
 
 static void o_shade(o_getblock_fn gb, const void* world, const float org[3], const float d0[3], int steps, const float sun[3],
-                    const int32_t* look, int shadow_steps, int liquid, float time, float out[4]) {
+                    const int32_t* look, int shadow_steps, int liquid, float time, float out[4], int* shadow_ray) {
     orayres R;
+    if (shadow_ray) *shadow_ray = 0;
     float dir[3];
     int nrefl;
     float m[3];
@@ -1535,6 +1536,7 @@ static void o_shade(o_getblock_fn gb, const void* world, const float org[3], con
                 orayres S;
                 o_cast(gb, world, so, sun, shadow_steps, &S);
                 dark = S.hit != 0;
+                if (shadow_ray) *shadow_ray = 1;
             }
         }
         if (dark)
@@ -1561,7 +1563,7 @@ static void* o_shade_worker(void* p) {
         int64_t pi = j->pix ? j->pix[k] : k;
         float d[3];
         o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
-        o_shade(o_gb_tree, j->t, j->org, d, j->steps, j->sun, j->look, j->shadow_steps, j->liquid, j->time, j->rgba + 4 * k);
+        o_shade(o_gb_tree, j->t, j->org, d, j->steps, j->sun, j->look, j->shadow_steps, j->liquid, j->time, j->rgba + 4 * k, NULL);
     }
     return NULL;
 }
@@ -1591,5 +1593,103 @@ EXPORT void orc_shade_frame(const otree* t, const float org[3], const float cam[
         pthread_create(&th[i], NULL, o_shade_worker, j);
     }
     for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(jobs);
+}
+
+/* §8(d) for the shading pass (bench.py --shade): node entries of every lookup the pass's rays make under
+   the same common-ancestor restart model as o_walk_entries — the primary ray with its reflections and
+   refractions (o_cast_refl: one lookup per DDA step, the DDA continuing after each bounce) and the 75-step
+   shadow ray of a lit, unreflected hit, which continues from the lookup state the primary left (as the AO
+   rays do, o_count_entries_ao).  The block each lookup returns is o_get_block's, so the walk is the shading
+   pass itself; the counter only rides along.  out[0] = entries, out[1] = shadow rays, out[2] = DDA lookups. */
+typedef struct {
+    const otree* t;
+    o_estate S;
+    uint64_t entries, lookups;
+} o_ecount;
+static int o_gb_count(const void* w, int x, int y, int z, uint32_t* f, uint64_t* c, float* m) {
+    o_ecount* E = (o_ecount*)w;
+    const otree* t = E->t;
+    o_estate* S = &E->S;
+    const int L = t->max_depth - 1;
+    const int r[3] = {x, y, z};
+    int n = 0;
+    if (S->have_prev) {
+        for (n = 0; n < L; n++) {
+            int off = 2 * (L - 1 - n);
+            if (o_child_index(r[0], r[1], r[2], off) != o_child_index(S->prev[0], S->prev[1], S->prev[2], off)) break;
+        }
+    }
+    if (n < S->depth) S->depth = n;
+    for (;;) {
+        const onode* nd = NODE(t, S->stack[S->depth]);
+        if (nd->flags & 1) break;
+        if (S->depth >= L) break;
+        int off = 2 * (L - 1 - S->depth);
+        int idx = o_child_index(r[0], r[1], r[2], off);
+        if (!((nd->w0 >> idx) & 1)) break;
+        S->stack[S->depth + 1] = ARR(t, nd->w1)->c[idx];
+        S->depth++;
+        E->entries++;
+    }
+    memcpy(S->prev, r, sizeof(r));
+    S->have_prev = 1;
+    E->lookups++;
+    return o_get_block(t, x, y, z, f, c, m);
+}
+typedef struct {
+    const otree* t;
+    float org[3], cam[3], ppx, ppy, rw, rh, sun[3], time;
+    int W, H, steps, shadow_steps, tid, nthreads, liquid;
+    const int64_t* pix;
+    int64_t n;
+    uint64_t out[3];
+} o_sejob;
+static void* o_shade_entries_worker(void* p) {
+    o_sejob* j = (o_sejob*)p;
+    for (int64_t k = j->tid; k < j->n; k += j->nthreads) {
+        int64_t pi = j->pix ? j->pix[k] : k;
+        float d[3], rgba[4];
+        o_pixel_dir(j->cam, j->ppx, j->ppy, j->rw, j->rh, (int)(pi % j->W), (int)(pi / j->W), d);
+        o_ecount E;
+        memset(&E, 0, sizeof(E));
+        E.t = j->t;
+        E.S.stack[0] = j->t->root;
+        int sh = 0;
+        o_shade(o_gb_count, &E, j->org, d, j->steps, j->sun, NULL, j->shadow_steps, j->liquid, j->time, rgba, &sh);
+        j->out[0] += E.entries;
+        j->out[1] += (uint64_t)sh;
+        j->out[2] += E.lookups;
+    }
+    return NULL;
+}
+EXPORT void orc_shade_entries(const otree* t, const float org[3], const float cam[3], float ppx, float ppy, int W, int H, int steps,
+                              const float sun[3], int shadow_steps, const int64_t* pix, int64_t n, int nthreads, int liquid, float time,
+                              uint64_t out[3]) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    o_sejob* jobs = (o_sejob*)calloc((size_t)nthreads, sizeof(o_sejob));
+    for (int i = 0; i < nthreads; i++) {
+        o_sejob* j = &jobs[i];
+        j->t = t;
+        memcpy(j->org, org, 12);
+        memcpy(j->cam, cam, 12);
+        memcpy(j->sun, sun, 12);
+        j->ppx = ppx; j->ppy = ppy;
+        j->rw = 1.0f / (float)W; j->rh = 1.0f / (float)H;
+        j->W = W; j->H = H; j->steps = steps; j->shadow_steps = shadow_steps;
+        j->liquid = liquid;
+        j->time = time;
+        j->pix = pix;
+        j->n = pix ? n : (int64_t)W * H;
+        j->tid = i; j->nthreads = nthreads;
+        pthread_create(&th[i], NULL, o_shade_entries_worker, j);
+    }
+    out[0] = out[1] = out[2] = 0;
+    for (int i = 0; i < nthreads; i++) {
+        pthread_join(th[i], NULL);
+        for (int k = 0; k < 3; k++) out[k] += jobs[i].out[k];
+    }
     free(jobs);
 }

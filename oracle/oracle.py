@@ -146,6 +146,8 @@ def lib(native=False):
                                     C.c_int, vp, vp]
     L.orc_shade_frame.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, _f32p, vp, C.c_int, vp, C.c_int64,
                                   C.c_int, vp, C.c_int, C.c_float]
+    L.orc_shade_entries.argtypes = [vp, _f32p, _f32p, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int, _f32p, C.c_int, vp, C.c_int64,
+                                    C.c_int, C.c_int, C.c_float, vp]
     L.orc_sin_f32.restype = C.c_float
     L.orc_sin_f32.argtypes = [C.c_float]
     _libs[path] = L
@@ -353,6 +355,19 @@ class Tree:
         n = W * H if pixels is None else len(pixels)
         pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
         return self.L.orc_frame_entries_ao(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, n_ao, ao_steps, _ptr(pix), n, nthreads)
+
+    def shade_entries(self, org, cam, W, H, steps, sun, shadow_steps=75, ppx=None, ppy=None, pixels=None, nthreads=8, liquid=False,
+                      time=0.0):
+        """§8(d) node entries of the shading pass (oracle.c orc_shade_entries): (entries, shadow rays, DDA lookups)
+        summed over the frame's pixels (or a subset)"""
+        if ppx is None:
+            ppx, ppy = proj_plane(W, H)
+        n = W * H if pixels is None else len(pixels)
+        pix = None if pixels is None else np.ascontiguousarray(pixels, dtype=np.int64)
+        out = np.zeros(3, np.uint64)
+        self.L.orc_shade_entries(self.h, f3(org), f3(cam), ppx, ppy, W, H, steps, f3(sun), shadow_steps, _ptr(pix), n, nthreads,
+                                 1 if liquid else 0, time, _ptr(out))
+        return int(out[0]), int(out[1]), int(out[2])
 
 
 class Dense:

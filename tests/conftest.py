@@ -42,3 +42,20 @@ def ref_world(rt):
 @pytest.fixture(scope="session")
 def ref_tree(ref_world):
     return ref_world.build()
+
+
+@pytest.fixture(scope="session")
+def depth12(rt):
+    # the tree bench.py times: noise + build on the GPU (svo_build_terrain_gpu), so the
+    # C3 / C4 / shaded parity tests pin the on-device builder to the oracle as well
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return rt.Tree.terrain_gpu(6, 4096, 4096, 0)
+
+
+@pytest.fixture(scope="session")
+def oracle12(oracle_mod):
+    # the oracle's reference-format (collapsed) depth-12 tree, built once for the C3 / C4 / shaded tests
+    return oracle_mod.Tree.terrain(6, 4096, 4096, nthreads=16)

@@ -401,19 +401,6 @@ def test_dense_grid_c1(rt, oracle_mod, torch_cuda, ref_world_oracle):
     assert np.array_equal(pc[np.where(out["hit"], out["material"], 0)], ref["color"])
 
 
-@pytest.fixture(scope="module")
-def depth12(rt, torch_cuda):
-    # the tree bench.py times: noise + build on the GPU (svo_build_terrain_gpu), so the
-    # C3 / C4 parity below pins the on-device builder to the oracle as well
-    return rt.Tree.terrain_gpu(6, 4096, 4096, 0)
-
-
-@pytest.fixture(scope="module")
-def oracle12(oracle_mod):
-    # the oracle's reference-format (collapsed) depth-12 tree, built once for the module's C3 / C4 tests
-    return oracle_mod.Tree.terrain(6, 4096, 4096, nthreads=16)
-
-
 def test_depth12_full_frame_parity(rt, depth12, oracle12):
     """C3: depth-12 terrain (4096^2 columns, 6 levels), the C1 pose, S = 16384; every pixel of the
     1080p frame against the oracle's reference-format tree, every field (the frame bench.py times)."""
@@ -602,16 +589,17 @@ def test_ao_plan_budgets(rt, gtree, ref_world_oracle, n_ao, ao_steps):
         assert np.array_equal(out["ao"], ao), (org, n_ao, ao_steps)
 
 
-def test_ao_depth12_full_frame(rt, depth12, oracle12):
-    """C4: the C3 frame + 16 hemisphere AO rays of 5 steps per hit; every pixel's AO count and hit
+@pytest.mark.parametrize("n_ao", [16, 20])
+def test_ao_depth12_full_frame(rt, depth12, oracle12, n_ao):
+    """C4: the C3 frame + 16 (and 20) hemisphere AO rays of 5 steps per hit; every pixel's AO count and hit
     flag against the oracle, and the per-face plan equal to tracing every AO ray (CAST_AO_TRACE)."""
     dn = rt.normalize([1, -0.45, 1])
-    out = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=16, ao_steps=5))
-    ao, hit = oracle12.cast_frame_ao((4, 90, 4), dn, 1920, 1080, 16384, 16, 5, nthreads=16)
+    out = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=n_ao, ao_steps=5))
+    ao, hit = oracle12.cast_frame_ao((4, 90, 4), dn, 1920, 1080, 16384, n_ao, 5, nthreads=16)
     assert np.array_equal(out["hit"], hit != 0)
     bad = np.nonzero(out["ao"] != ao)[0]
     assert len(bad) == 0, "AO differs at %d pixels, first %s: gpu %s oracle %s" % (len(bad), bad[:5], out["ao"][bad[:5]], ao[bad[:5]])
-    tr = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=16, ao_steps=5, flags=rt.CAST_AO_TRACE))
+    tr = rt.decode_hits(depth12.cast_frame((4, 90, 4), dn, 1920, 1080, 16384, ao_samples=n_ao, ao_steps=5, flags=rt.CAST_AO_TRACE))
     assert np.array_equal(out["ao"], tr["ao"])  # plan == traced AO rays over the whole frame
     assert out["ao"].mean() > 0.5  # terrain occludes part of the hemisphere
 
@@ -630,6 +618,13 @@ def test_depth14_4k_sampled_parity(rt, oracle_mod, torch_cuda):
     assert ref["rc"] == 0
     assert np.array_equal(out["pos"][pix], ref["pos"]) and np.array_equal(out["steps"][pix], ref["steps"])
     assert np.array_equal(out["hit"][pix], ref["hit"] != 0)
+    assert np.array_equal(out["last_pos"][pix], ref["last"])
+    # the block at pos: palette flags and colour (ray_caster.cpp:83) against the oracle's getBlock
+    pal = t.palette()
+    pf = np.array([p[0] for p in pal], np.uint32)
+    pc = np.array([p[1] for p in pal], np.uint64)
+    mid = np.where(out["hit"][pix], out["material"][pix], 0)
+    assert np.array_equal(pf[mid], ref["flags"]) and np.array_equal(pc[mid], ref["color"])
     assert np.array_equal(out["t"][pix], ref["t"].astype(np.float32))
     assert np.abs(out["pos"][:, [0, 2]]).max() < 4096  # the premise of the 4096^2 oracle
     del t

@@ -99,9 +99,12 @@ def test_pick_ray_on_device(rt, gtree, torch_cuda):
             s.synchronize()
             r = rec[:7].cpu().numpy()
             assert tuple(r[:3]) == tuple(pos) and tuple(r[3:6]) == tuple(last) and r[6] == left, (org, cd, steps, r, pos, last, left)
-    org, cd = CAMERAS[0]
+    # a pose whose 30-step pick ray lands on terrain in view (the reference default camera's pick walks +z only, into
+    # air: its highlight never shows); the oracle highlights 531 pixels of this frame
+    org, cd = (35.0, 50.0, 35.0), (1.0, -1.0, 1.0)
     cam_dir = rt.normalize(cd)
-    (pos, _, _), _ = gtree.cast_ray_from_cam(org, cam_dir, 30)
+    (pos, _, left), _ = gtree.cast_ray_from_cam(org, cam_dir, 30)
+    assert tuple(pos) == (39, 44, 40) and left == 15
     d = gtree.frame_desc(org, cam_dir, 160, 90, 300)
     a = torch.empty((160 * 90, 4), dtype=torch.float32, device="cuda")
     b = torch.empty_like(a)
@@ -113,7 +116,7 @@ def test_pick_ray_on_device(rt, gtree, torch_cuda):
         gtree.shade(d, none, sun=rt.sun_dir(), stream=s)
     s.synchronize()
     assert torch.equal(a, b)
-    assert not torch.equal(a, none)  # the looked-at voxel is in view and highlighted
+    assert int((a != none).any(1).sum()) > 100  # the looked-at voxel is in view and highlighted
 
 
 def test_shade_other_suns(rt, gtree, ref_world_oracle):
@@ -272,3 +275,25 @@ def test_shade_escape_is_exact(rt, gtree, lake_scene, cam):
         f2, _ = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir(), with_hits=True)
         g2 = gtree.shade_frame(org, cam_dir, 200, 120, S, sun=rt.sun_dir())
         assert np.array_equal(f2.cpu().numpy(), g2.cpu().numpy()), (cam, S)
+
+
+def test_shade_bench_scene_full_frame(rt, depth12, oracle12, torch_cuda):
+    """The shaded workload bench.py --shade times, every pixel: the GPU-built 4096^2-column solid and full-view
+    (water) trees, the C3 pose, S = 16384, the reference sun; the image without hit records (the bench's form:
+    escaping rays stop early) against the oracle's liquid mode over the whole 1080p frame (low_res.frag:139-252,
+    319-391), equal to the image rendered with hit records, and the water is exercised (refracted rays travel
+    4x further before wrapping than on the 1024^2 scenes above)."""
+    torch = torch_cuda
+    scene = rt.Tree.terrain_gpu(6, 4096, 4096, 0, view=rt.VIEW_ALL)
+    org, cam_dir = (4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0))
+    W, H, S = 1920, 1080, 16384
+    img = depth12.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), scene=scene)
+    rgba, hits = depth12.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), with_hits=True, scene=scene)
+    assert torch.equal(img, rgba)  # escape is exact
+    ref = oracle12.shade_frame(org, cam_dir, W, H, S, rt.sun_dir(), liquid=True, nthreads=16)
+    hit = rt.decode_hits(hits)["hit"]
+    _check(img, ref, hit, "bench scene")
+    dry = depth12.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir())
+    wet = int((dry != img).any(1).sum().item())
+    assert wet > 100000, wet  # lake pixels: tinted and refracted
+    del scene
