@@ -167,6 +167,10 @@ int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* lev
    svo_tree_ceilings' layout and their uint32 pairs (low: the block's ceiling, high: its next-level block's; the
    last level paired with itself).  levels = 0 when the tree has none.  Either buffer may be NULL. */
 int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32_t* pairs, int64_t cap, int32_t* levels, int64_t* n);
+/* The per-level quads in HBM (the shading pass's walk over every ceiling level): for every block of the finest
+   level (4^SVO_CEIL_K0 columns, row-major [z][x]), the ceilings of the blocks of levels 0..3 holding it, int16 each,
+   level j in bits 16j..16j+15 (a level the tree lacks: 0x7FFF).  quads may be NULL (count only); n = elements. */
+int svo_tree_device_ceiling_quads(const svo_tree* t, uint64_t* quads, int64_t cap, int64_t* n);
 /* Checkpoint (the reference regenerates its world at every start, main.cpp:190): write the
    linearised tree (levels, view, palette, nodes, material runs; a checksum) to `path`, and read it back
    as a new tree (not uploaded).  Loading validates every child / material reference against the array

@@ -46,7 +46,7 @@ STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "bric
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
               "no_progress", "root_starts", "cache_empty", "wave_skips", "wave_descents",
-              "path_starts", "ao_node_loads", "ceil_moves", "iters_above_top", "bends")  # wave_*: per wave (64 rays)
+              "path_starts", "ao_node_loads", "ceil_moves", "iters_above_top", "bends", "tints", "tint_iters")  # wave_*: per wave (64 rays)
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: the larger wire record (12 B general, 8 B compact: Tree.wire_bytes(desc))
@@ -141,7 +141,7 @@ ABI_SYMBOLS = (
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
-    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_cast_ray_from_cam_async",
+    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_cast_ray_from_cam_async",
 )
 
 
@@ -184,6 +184,7 @@ def lib():
                      ("svo_tree_ceilings", [vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
                      ("svo_tree_guard_trips", [vp, C.POINTER(C.c_uint64), i32]),
                      ("svo_tree_device_ceilings", [vp, vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
+                     ("svo_tree_device_ceiling_quads", [vp, vp, C.c_int64, C.POINTER(C.c_int64)]),
                      ("svo_cast_ray_from_cam_async", [vp, f3, f3, i32, vp, vp])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
@@ -652,6 +653,15 @@ class Tree:
         _check(lib().svo_tree_device_ceilings(self._h, c.ctypes.data_as(C.c_void_p), p.ctypes.data_as(C.c_void_p), n.value, C.byref(lv),
                                               C.byref(n)), "svo_tree_device_ceilings")
         return lv.value, c, p
+
+    def device_ceiling_quads(self):
+        """uint64 quads of the finest ceiling blocks in HBM: the ceilings of levels 0..3 holding each (svo_tree_device_ceiling_quads)"""
+        n = C.c_int64()
+        _check(lib().svo_tree_device_ceiling_quads(self._h, None, 0, C.byref(n)), "svo_tree_device_ceiling_quads")
+        q = np.zeros(n.value, np.uint64)
+        _check(lib().svo_tree_device_ceiling_quads(self._h, q.ctypes.data_as(C.c_void_p), n.value, C.byref(n)),
+               "svo_tree_device_ceiling_quads")
+        return q
 
     def guard_trips(self, reset=False):
         """Rays of launches over this tree that ended on the progress guard (svo_tree_guard_trips): 0 unless a

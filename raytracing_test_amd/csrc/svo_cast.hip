@@ -96,6 +96,7 @@ struct CastParams {
     uint32_t ceil_sh[2];
     int64_t ceil_off[2];
     const uint32_t* ceilp;  // the launch's two levels paired (svo_tree.d_ceilp at its first level's offset)
+    const uint64_t* ceilq;  // every level per finest block (svo_tree.d_ceilq; trace CEIL == 2)
     uint32_t* guard_trips;  // the tree's counter of progress-guard trips (svo_tree_guard_trips)
 };
 
@@ -473,6 +474,7 @@ struct Stats {
     uint32_t iters;                                // this lane's traversal iterations
     uint32_t above_top;                            // iterations that start above the tree's highest stored row
     uint32_t bends;                                // reflections and refractions (shading)
+    uint32_t tints, tint_iters;                    // refractive voxels passed; iterations that ended passing one
 };
 
 // true on one lane of the active lanes (wave-level counters)
@@ -764,13 +766,15 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // (lookup: PSH) — a ray ending in a SOLID region above the bricks leaves that region's mask and ref
 // ESCAPE (shading rays whose end position is not output): a ray moving up above the highest stored
 // voxel row `top` (wrapped) whose budget cannot carry it past the extent in y leaves the loop as a
-// miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off).
+// miss at once — it can only enter empty space — and skips its remaining steps (top < 0: off); so does
+// a ray whose budget ends inside an empty box; and with CEIL, a ray above `top` crosses the whole
+// half-space above it (every x and z) in one move.
 // DIRS (1..8): every ray of the launch steps with the signs dirs_sign(DIRS, k) (frame_dirs proves it
 // on the host): the steps are compile-time constants and the sign branches of the crossings and brick
 // walks fold away; 0: per-wave sign flags (dir_flags)
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
-template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, bool CEIL = false,
+template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, int CEIL = 0,
           class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
@@ -844,7 +848,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the hit is mat != kNoHit (a flag of its own costs lane-mask upkeep every iteration)
     uint32_t mat = kNoHit;
     const uint32_t wm = P.wmask;
-    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
     // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
     // the whole world = node 0): the first lookup takes the same path as every later one
@@ -871,8 +875,11 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // coordinate bits changed since the last voxel known to lie in the parent's region, by ceiling moves since
     // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
-    const bool ceil_on = CEIL && P.ceil_levels > 0;  // (uniform)
+    // CEIL 1: the launch's two levels of the column ceilings (P.ceilp pairs); 2: every level, the coarsest block the ray is
+    // above (P.ceilq: a max-mipmap walk of the ceilings)
+    const bool ceil_on = CEIL != 0 && P.ceil_levels > 0;  // (uniform)
     uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 16-column block (key) and its ceilings (c0 | c1 << 16)
+    uint64_t cq = 0ull;                      // (CEIL 2: the ceilings of the blocks of every level holding the lane's 16-column block)
     while (!done) {
         // the voxel just entered is untested
         if (STATS) {
@@ -898,9 +905,24 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         // whole block: that box is crossed without a lookup (R_CEIL; the next lookup restarts from the
         // per-lane path at the depth the moves since the last lookup left intact)
         int32_t cex[3] = {0, 0, 0};
-        bool cl = false, any_cl = false;
+        bool cl = false, any_cl = false, gt = false;
         int32_t c0 = -1, c1 = 32767;  // the ceilings of the lane's blocks at the launch's two levels (set_ceilings)
-        if (ceil_on && fast && R.steps > 0) {
+        uint32_t lv = 0u;             // (CEIL 2) how many levels' ceilings the ray is above: its box is a block of level lv - 1
+        if (CEIL == 2 && ceil_on && fast && R.steps > 0) {
+            const int32_t y = (int32_t)w[1];
+            constexpr uint32_t lsh0 = 2u * kCeilK0;
+            const uint32_t rows0 = (wm + 1u) >> lsh0;
+            const uint32_t key = __umul24(w[2] >> lsh0, rows0) + (w[0] >> lsh0);
+            if (key != ckey) {
+                ckey = key;
+                cq = P.ceilq[key];
+            }
+            // (the ceilings grow with the level: a block's holds its children's)
+            lv = (uint32_t)(y > (int32_t)(int16_t)cq) + (uint32_t)(y > (int32_t)(int16_t)(cq >> 16)) +
+                 (uint32_t)(y > (int32_t)(int16_t)(cq >> 32)) + (uint32_t)(y > (int32_t)(int16_t)(cq >> 48));
+            cl = lv != 0u;
+            if (ESCAPE) gt = top >= 0 && y > top;
+        } else if (ceil_on && fast && R.steps > 0) {
             const int32_t y = (int32_t)w[1];
             const uint32_t lsh0 = P.ceil_sh[0], rows0 = (wm + 1u) >> lsh0;
             const uint32_t key = __umul24(w[2] >> lsh0, rows0) + (w[0] >> lsh0);  // (< 2^28: 2^14 x 2^14 blocks at most)
@@ -914,6 +936,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             c1 = (int32_t)cval >> 16;
             const bool p1 = y > c1;
             cl = p1 || y > c0;
+            // above the tree's highest stored row (ESCAPE instances: top): every column is empty from there up to the
+            // top of the world, so the box spans every x and z (a ray climbing out of the terrain band crosses it in one
+            // move instead of one per 256-column block; its budget ends in it or it wraps in y)
+            if (ESCAPE) gt = top >= 0 && y > top;
         }
         // (the box exits are taken only when a lane of the wave moves — wave-uniform; with the forward boxes gated
         // the same way, 1.1 % faster at C3 than per-lane selects: profiles/r03/ab_r03_x_*.log)
@@ -921,13 +947,18 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         if (any_cl) {
             const int32_t y = (int32_t)w[1];
             const bool p1 = y > c1;
-            const uint32_t bmk = (1u << (p1 ? P.ceil_sh[1] : P.ceil_sh[0])) - 1u;  // block width - 1
-            const int32_t c = p1 ? c1 : c0;
+            uint32_t bmk = (1u << (p1 ? P.ceil_sh[1] : P.ceil_sh[0])) - 1u;  // block width - 1
+            int32_t c = p1 ? c1 : c0;
+            if (CEIL == 2) {
+                const uint32_t l = (lv - 1u) & 3u;  // (lanes with lv 0 take no box)
+                bmk = (1u << (2u * (kCeilK0 + l))) - 1u;
+                c = (int32_t)(int16_t)(cq >> (16u * l));
+            }
             // steps to leave the box, less one: the block's faces in x / z, the ceiling (down) or the top
             // of the world (up) in y
-            cex[0] = (int32_t)(R.s[0] > 0 ? bmk - (w[0] & bmk) : (w[0] & bmk));
-            cex[1] = R.s[1] < 0 ? y - c - 1 : (int32_t)(wm - w[1]);
-            cex[2] = (int32_t)(R.s[2] > 0 ? bmk - (w[2] & bmk) : (w[2] & bmk));
+            cex[0] = gt ? R.steps : (int32_t)(R.s[0] > 0 ? bmk - (w[0] & bmk) : (w[0] & bmk));
+            cex[1] = R.s[1] < 0 ? y - (gt ? top : c) - 1 : (int32_t)(wm - w[1]);
+            cex[2] = gt ? R.steps : (int32_t)(R.s[2] > 0 ? bmk - (w[2] & bmk) : (w[2] & bmk));
         }
         uint32_t kind = R_CEIL;
         if (!cl) {
@@ -971,6 +1002,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             if (STATS && fast) st.skip_out++;
             if (fast) {
                 done = true;  // the budget ends inside this empty box: steps after the loop
+                // (ESCAPE: where a ray without a hit ends is not output — a miss whose budget ends in empty space skips them)
+                if (ESCAPE && top >= 0) escaped = true;
             } else {
                 // not exact: voxel steps to the end of this (empty) 4^3 brick, then a lookup
                 pend = true;
@@ -1036,6 +1069,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // a negative step, then min(new step, 0); deltaPos restarts from the current cell.
             const bool liquid = (mfl & 0x10u) != 0u;
             const float t0 = liquid ? 0.94f : 0.95f, t1 = liquid ? 0.97f : 0.95f, t2 = liquid ? 1.0f : 0.95f;
+            if (STATS) {
+                st.tints++;
+                st.tint_iters++;
+            }
             bounce->m[0] *= t0;
             bounce->m[1] *= t1;
             bounce->m[2] *= t2;
@@ -1101,6 +1138,38 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
                     bounce->m[0] *= t0;
                     bounce->m[1] *= t1;
                     bounce->m[2] *= t2;
+                    if (STATS) st.tints++;
+                    dda_step(R);
+                }
+            } else if (kind == R_BRICK) {
+                // the rest of the brick (a lake's surface layer: water and air in one brick): its voxel mask and
+                // materials are at hand, so refractive voxels are passed (each tints with its own block) and empty
+                // ones stepped without lookups; any other block ends the ray there (a mirror with budget left is
+                // left to the next iteration, which reflects it), and leaving the brick ends the pass (a lookup)
+                for (;;) {
+                    uint32_t w[3];
+                    wrap3(R, wm, w);
+                    if (((w[0] ^ wr[0]) | (w[1] ^ wr[1]) | (w[2] ^ wr[2])) >> 2) break;
+                    const uint32_t v = child_slot(w[0], w[1], w[2], 0u);
+                    if ((bmask >> v) & 1ull) {
+                        const uint32_t m2 = brick_material(mats, bmask, bref, binfo, v);
+                        const uint32_t f2 = P.mat_flags[m2];
+                        if ((f2 & 7u) != 5u || R.steps <= 0) {
+                            if ((f2 & 7u) != 3u || R.steps <= 0) {
+                                mat = m2;  // the hit
+                                done = true;
+                            }
+                            break;
+                        }
+                        const bool lq = (f2 & 0x10u) != 0u;
+                        bounce->m[0] *= lq ? 0.94f : 0.95f;
+                        bounce->m[1] *= lq ? 0.97f : 0.95f;
+                        bounce->m[2] *= lq ? 1.0f : 0.95f;
+                        if (STATS) st.tints++;
+                    } else if (R.steps <= 0) {
+                        done = true;  // the budget ends in an empty voxel
+                        break;
+                    }
                     dda_step(R);
                 }
             }
@@ -1155,6 +1224,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         atomicAdd(P.stats + 23, (unsigned long long)st.ceil_moves);
         atomicAdd(P.stats + 24, (unsigned long long)st.above_top);
         atomicAdd(P.stats + 25, (unsigned long long)st.bends);
+        atomicAdd(P.stats + 26, (unsigned long long)st.tints);
+        atomicAdd(P.stats + 27, (unsigned long long)st.tint_iters);
         // per-ray work (offline analysis, bench.py SVO_RAY_WORK): 16-bit fields, lookups | iterations | brick steps | node loads
         if (ray_work)
             *ray_work = (unsigned long long)min(st.lookups, 65535u) | ((unsigned long long)min(st.iters, 65535u) << 16) |
@@ -1372,7 +1443,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
     }
     if (SHADE && out >= 0) {
         Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
-        const Hit h = trace<STATS, true, true, SEG, 0, false, true>(
+        const Hit h = trace<STATS, true, true, SEG, 0, false, 2>(
             P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
             &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
         if (P.pos) {
@@ -1423,7 +1494,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
         P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
     } else if (out >= 0) {
         Parent pfin;
-        const Hit h = trace<STATS, false, false, SEG, DIRS, AO, true>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
+        const Hit h = trace<STATS, false, false, SEG, DIRS, AO, 1>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
         if (!SHADE && P.wire) {  // (wave-uniform: one launch writes one kind of record)
             wire_put(P.wire, P.wire_compact != 0, out, o, h.x, h.y, h.z, h.t, h.info);
@@ -1667,8 +1738,9 @@ static void frame_axes(CastParams& P, int dirs) {
 
 // The two ceiling levels a launch checks, as levels of the tree's table (4^(kCeilK0 + j) columns per block).
 // Primary casts: 16 and 64 columns (C3 0.1824 -> 0.1787 ms, C5 0.562 -> 0.543 against 64 / 256; 16 / 256 was
-// slower than both: profiles/r03/ab_j_*.log).  Shading: 64 and 256 (16 / 64 measured 0.62 -> 0.80 ms there).
-constexpr int kCeilPrimary[2] = {0, 1}, kCeilShade[2] = {1, 2};
+// slower than both: profiles/r03/ab_j_*.log).  The shading pass walks every level (trace CEIL 2: P.ceilq); its
+// pair levels are unused.
+constexpr int kCeilPrimary[2] = {0, 1}, kCeilShade[2] = {0, 1};
 
 static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& P, const int lv[2]) {
     P.ceil = nullptr;
@@ -1678,6 +1750,7 @@ static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& 
     P.ceil_levels = t->ceil_levels > lv[1] ? 2 : (t->ceil_levels > lv[0] ? 1 : 0);
     // (the pair table of level lv[0] holds lv[0] + 1 = lv[1] when the tree has it, else lv[0] itself — as below)
     P.ceilp = P.ceil_levels > 0 ? reinterpret_cast<const uint32_t*>(t->d_ceilp) + t->ceilp_off[lv[0]] : nullptr;
+    P.ceilq = P.ceil_levels > 0 ? reinterpret_cast<const uint64_t*>(t->d_ceilq) : nullptr;
     for (int j = 0; j < 2; j++) {
         // (one level only: the second is a copy of the first, so the kernel may read both unconditionally)
         const int l = j < P.ceil_levels ? lv[j] : lv[0];
@@ -1770,7 +1843,8 @@ void svo::tree_release_device(svo_tree* t) {
     if (t->d_ao_plan) (void)hipFree(t->d_ao_plan);
     if (t->d_ceil) (void)hipFree(t->d_ceil);
     if (t->d_ceilp) (void)hipFree(t->d_ceilp);
-    t->d_ceil = t->d_ceilp = nullptr;
+    if (t->d_ceilq) (void)hipFree(t->d_ceilq);
+    t->d_ceil = t->d_ceilp = t->d_ceilq = nullptr;
     t->ceil_levels = 0;
     t->ceil_dev_n = 0;
     t->d_ao_plan = nullptr;
@@ -1809,7 +1883,29 @@ static void ceil_pairs(svo_tree* t, int32_t n, int64_t x0, int64_t z0, int64_t x
     }
 }
 
-// the column ceilings of the host image (tree_ceilings) and their pairs, replacing the device copies (the device
+// The ceiling quads (svo_tree.d_ceilq) of the level-0 blocks holding columns [x0, x1) x [z0, z1), widened to whole blocks of
+// the coarsest level (whose change reaches every level-0 block inside it).  Returns the first and last row written.
+static void ceil_quads(svo_tree* t, int32_t n, int64_t x0, int64_t z0, int64_t x1, int64_t z1, int64_t zr[2]) {
+    const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0));
+    const int32_t tsh = 2 * (n - 1);  // the coarsest level's blocks, in level-0 blocks (log2)
+    const int32_t bsh = 2 * kCeilK0 + tsh;
+    const int64_t bz0 = (z0 >> bsh) << tsh, bz1 = std::min(rows, (((z1 - 1) >> bsh) + 1) << tsh);
+    const int64_t bx0 = (x0 >> bsh) << tsh, bx1 = std::min(rows, (((x1 - 1) >> bsh) + 1) << tsh);
+    const int16_t* c = t->ceil_host.data();
+    for (int64_t z = bz0; z < bz1; z++)
+        for (int64_t x = bx0; x < bx1; x++) {
+            uint64_t q = 0;
+            for (int32_t j = 0; j < kCeilMax; j++) {
+                const int16_t v = j < n ? c[t->ceil_off[j] + (z >> (2 * j)) * (rows >> (2 * j)) + (x >> (2 * j))] : (int16_t)0x7FFF;
+                q |= (uint64_t)(uint16_t)v << (16 * j);
+            }
+            t->ceilq_host[z * rows + x] = q;
+        }
+    zr[0] = bz0;
+    zr[1] = bz1;
+}
+
+// the column ceilings of the host image (tree_ceilings), their pairs and quads, replacing the device copies (the device
 // buffers are kept when their size is unchanged)
 static int upload_ceilings(svo_tree* t) {
     int32_t n = 0;
@@ -1819,20 +1915,26 @@ static int upload_ceilings(svo_tree* t) {
         n = tree_ceilings(t, t->ceil_host, off);
         for (int j = 0; j < kCeilMax; j++) t->ceil_off[j] = t->ceilp_off[j] = off[j];
         t->ceilp_host.assign(t->ceil_host.size(), 0u);
+        t->ceilq_host.clear();
         if (n > 0) {
             const int64_t e = (int64_t)1 << (2 * t->levels);
             ceil_pairs(t, n, 0, 0, e, e, zr);
+            t->ceilq_host.assign((size_t)1 << (4 * (t->levels - kCeilK0)), 0ull);
+            int64_t qr[2];
+            ceil_quads(t, n, 0, 0, e, e, qr);
         }
     } catch (const std::bad_alloc&) {
         t->ceil_host.clear();
         t->ceilp_host.clear();
+        t->ceilq_host.clear();
         n = -1;
     }
     t->ceil_dirty.clear();
     if (n <= 0 || (int64_t)t->ceil_host.size() != t->ceil_dev_n) {
         if (t->d_ceil) (void)hipFree(t->d_ceil);
         if (t->d_ceilp) (void)hipFree(t->d_ceilp);
-        t->d_ceil = t->d_ceilp = nullptr;
+        if (t->d_ceilq) (void)hipFree(t->d_ceilq);
+        t->d_ceil = t->d_ceilp = t->d_ceilq = nullptr;
         t->ceil_dev_n = 0;
     }
     t->ceil_levels = 0;
@@ -1842,10 +1944,12 @@ static int upload_ceilings(svo_tree* t) {
     if (!t->d_ceil) {
         HIP_TRY(hipMalloc(&t->d_ceil, m * sizeof(int16_t)), SVO_ENOMEM);
         HIP_TRY(hipMalloc(&t->d_ceilp, m * sizeof(uint32_t)), SVO_ENOMEM);
+        HIP_TRY(hipMalloc(&t->d_ceilq, t->ceilq_host.size() * sizeof(uint64_t)), SVO_ENOMEM);
         t->ceil_dev_n = (int64_t)m;
     }
     HIP_TRY(hipMemcpy(t->d_ceil, t->ceil_host.data(), m * sizeof(int16_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     HIP_TRY(hipMemcpy(t->d_ceilp, t->ceilp_host.data(), m * sizeof(uint32_t), hipMemcpyHostToDevice), SVO_EDEVICE);
+    HIP_TRY(hipMemcpy(t->d_ceilq, t->ceilq_host.data(), t->ceilq_host.size() * sizeof(uint64_t), hipMemcpyHostToDevice), SVO_EDEVICE);
     t->ceil_levels = n;
     return SVO_OK;
 }
@@ -1862,12 +1966,20 @@ static int sync_ceilings(svo_tree* t) {
     std::vector<std::array<int64_t, 4>> rects;
     rects.swap(t->ceil_dirty);
     for (const auto& r : rects) {
-        int64_t zr[kCeilMax][2];
+        int64_t zr[kCeilMax][2], qr[2];
         try {
             ceilings_update_rect(t, t->ceil_host, t->ceil_off, n, r[0], r[1], r[2], r[3]);
             ceil_pairs(t, n, r[0], r[1], r[2], r[3], zr);
+            ceil_quads(t, n, r[0], r[1], r[2], r[3], qr);
         } catch (const std::bad_alloc&) {
             SVO_FAIL(SVO_ENOMEM, "svo_tree_sync: column ceilings: out of host memory");
+        }
+        {
+            const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0));
+            const int64_t lo = qr[0] * rows, cnt = (qr[1] - qr[0]) * rows;
+            if (cnt > 0)
+                HIP_TRY(hipMemcpy(reinterpret_cast<uint64_t*>(t->d_ceilq) + lo, t->ceilq_host.data() + lo, cnt * sizeof(uint64_t),
+                                  hipMemcpyHostToDevice), SVO_EDEVICE);
         }
         for (int32_t j = 0; j < n; j++) {
             const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
@@ -2202,6 +2314,17 @@ extern "C" int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     if (ceil) HIP_TRY(hipMemcpy(ceil, t->d_ceil, *n * sizeof(int16_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
     if (pairs) HIP_TRY(hipMemcpy(pairs, t->d_ceilp, *n * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
+    return SVO_OK;
+}
+
+extern "C" int svo_tree_device_ceiling_quads(const svo_tree* t, uint64_t* quads, int64_t cap, int64_t* n) {
+    if (!t || !n) SVO_FAIL(SVO_EINVAL, "svo_tree_device_ceiling_quads: NULL argument");
+    if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_device_ceiling_quads: tree not uploaded (svo_upload)");
+    *n = t->ceil_levels > 0 && t->d_ceilq ? (int64_t)t->ceilq_host.size() : 0;
+    if (quads && cap < *n) SVO_FAIL(SVO_ERANGE, "svo_tree_device_ceiling_quads: buffer too small");
+    if (*n == 0 || !quads) return SVO_OK;
+    HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    HIP_TRY(hipMemcpy(quads, t->d_ceilq, *n * sizeof(uint64_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
     return SVO_OK;
 }
 

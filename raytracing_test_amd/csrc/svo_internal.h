@@ -82,6 +82,11 @@ struct svo_tree {
     // its level-(j+1) block (high 16 bits; the last level repeats its own), uint32 at element ceilp_off[j] of d_ceilp
     void* d_ceilp = nullptr;
     int64_t ceilp_off[4] = {0, 0, 0, 0};
+    // every level at once for the finest level's blocks (the shading pass's max-mipmap walk): for each level-0 block, the
+    // ceilings of the blocks of levels 0..3 holding it, int16 each (level j in bits 16j .. 16j+15; a level the tree lacks:
+    // 0x7FFF, which no row is above), uint64 row-major [z][x] in d_ceilq
+    void* d_ceilq = nullptr;
+    std::vector<uint64_t> ceilq_host;
     int64_t ceil_dev_n = 0;            // elements of the d_ceil / d_ceilp allocations
     std::vector<int16_t> ceil_host;    // the host copies of d_ceil / d_ceilp (svo_tree_sync updates them in place)
     std::vector<uint32_t> ceilp_host;

@@ -65,7 +65,10 @@ def test_roofline_model_and_counters(bench):
     rf = bench.roofline(_args(), cfg, 2073600, 0.05e-3, 1)
     assert rf["frac"] is None and "withheld" in rf["note"]
     rs = bench.roofline(_args(shade=True), cfg, 2073600, 1.3e-3, 1)
-    assert rs["frac"] is None and rs["bytes_per_ray"] is None
+    # the shading pass: priced by its own §8(d) entries (oracle/bray.py C3_shade)
+    sb = bray["C3_shade"]
+    assert abs(rs["bytes_per_ray"] - sb["bytes_per_ray"]) < 0.01 and "shading pass" in rs["bytes_model"]
+    assert abs(rs["frac"] - sb["bytes_per_ray"] * 2073600 / 1.3e-3 / 1e9 / 8000.0) < 1e-4
     # counters measured at N = 1 scale per ray to another launch size (a rank's shard)
     rh = bench.roofline(_args(), cfg, 2073600 // 2, 0.12e-3, 2)
     assert rh["traffic"] == round(pmc["hbm_bytes_per_launch"] / 2)

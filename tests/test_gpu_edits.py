@@ -128,6 +128,23 @@ def _pairs_of(c, E, k0, lv):
     return p
 
 
+def _quads_of(c, E, k0, levels):
+    """tests' restatement of svo_tree.d_ceilq: per finest block, the ceilings of the blocks of levels 0..3 holding it"""
+    rows0 = E >> (2 * k0)
+    q = np.zeros((rows0, rows0), np.uint64)
+    o = 0
+    for j in range(4):
+        if j < levels:
+            rows = rows0 >> (2 * j)
+            lvl = c[o:o + rows * rows].reshape(rows, rows).astype(np.uint16).astype(np.uint64)
+            o += rows * rows
+            v = np.repeat(np.repeat(lvl, 1 << (2 * j), 0), 1 << (2 * j), 1)
+        else:
+            v = np.full((rows0, rows0), 0x7FFF, np.uint64)
+        q |= v << np.uint64(16 * j)
+    return q.reshape(-1)
+
+
 def test_sync_updates_device_ceilings_incrementally(rt, torch_cuda):
     """svo_tree_sync recomputes only the edited columns' ceilings and uploads their rows into the
     device tables already there.  After every edit + sync the tables in HBM equal a full recomputation over
@@ -157,6 +174,7 @@ def test_sync_updates_device_ceilings_incrementally(rt, torch_cuda):
         full = np.concatenate([x.reshape(-1) for x in tree.ceilings()])
         assert lv == lv0 and np.array_equal(c, full), "step %d: device ceilings differ from a full recomputation" % step
         assert np.array_equal(p, _pairs_of(full, E, rt.CEIL_K0, lv)), "step %d: pair table" % step
+        assert np.array_equal(tree.device_ceiling_quads(), _quads_of(full, E, rt.CEIL_K0, lv)), "step %d: quads" % step
     tree.sync()  # nothing changed: no-op
     assert np.array_equal(tree.device_ceilings()[1], c)
     print("edit + sync of 30-60 blocks: %s ms" % ", ".join("%.2f" % (x * 1e3) for x in times))

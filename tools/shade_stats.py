@@ -36,6 +36,15 @@ def main():
                      "brick_steps": round(float(brick[sel].mean()), 2), "loads": round(float(loads[sel].mean()), 2),
                      "iters_p50_90_99": np.percentile(iters[sel], [50, 90, 99]).round(1).tolist(),
                      "share_of_iters": round(float(iters[sel].sum() / iters.sum()), 4)}
+    # the long tail: bent rays at or above their 99th iteration percentile — where they end, how far they went
+    sel = bent & (iters >= np.percentile(iters[bent], 99))
+    used = np.where(g["hit"], S - g["steps"], S)
+    res["bent_tail"] = {"n": int(sel.sum()), "hit_frac": round(float(g["hit"][sel].mean()), 3),
+                        "steps_used_p50_90": np.percentile(used[sel], [50, 90]).round(0).tolist(),
+                        "end_y_p10_50_90": np.percentile(g["pos"][sel][:, 1], [10, 50, 90]).round(0).tolist(),
+                        "lookups": round(float(look[sel].mean()), 1), "brick_steps": round(float(brick[sel].mean()), 1),
+                        "prim_y_p50": float(np.median(prim["pos"][sel][:, 1])), "pixel_rows_p10_50_90":
+                        np.percentile(np.nonzero(sel)[0] // W, [10, 50, 90]).round(0).tolist()}
     fp = iters.reshape(H // 4, 4, W // 16, 16).transpose(0, 2, 1, 3).reshape(-1, 64).astype(np.float64)
     res["wave_iters_mean_of_max"] = round(float(fp.max(1).mean()), 2)
     res["lane_eff_iters"] = round(float(fp.mean() / fp.max(1).mean()), 4)
