@@ -1365,6 +1365,94 @@ __device__ __forceinline__ uint32_t ao_count_plan(const CastParams& P, const Mem
 }
 
 // WIDE: 64-bit node addresses (trees above kNarrowNodes nodes, or SVO_CAST_WIDE_ADDR)
+// The shading of a finished ray (low_res.frag:319-391 over castRayFromCam hits): its hit record (when requested) and its
+// colour — the looked-at highlight, the sky of its final direction, or the lit / shadowed block (a 75-step shadow ray
+// from the centre of lastPos through the solid view, smem); bn: its reflections / refraction (Bounce).  DIRS: the sun's
+// step octant (0: per-wave sign flags)
+template <int DIRS, class Mem>
+__device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, const Path& path, const Hit& h, const Bounce& bn, int64_t out) {
+        if (P.pos) {
+        reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
+        P.t[out] = h.t;
+        P.info[out] = h.info;
+    }
+    const bool hit = (h.info & HIT_BIT) != 0u;
+    const float* m = bn.m;  // finalColorMod
+    float3 c;
+    int32_t lk[3] = {P.look[0], P.look[1], P.look[2]};
+    bool lv = P.look_valid != 0;
+    if (P.look_dev) {  // (uniform: the pick ray's record, written on this stream before the launch)
+        lk[0] = P.look_dev[0];
+        lk[1] = P.look_dev[1];
+        lk[2] = P.look_dev[2];
+        lv = true;
+    }
+    if (lv && h.x == lk[0] && h.y == lk[1] && h.z == lk[2]) {
+        const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
+        c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
+    } else if (!hit) {
+        const float3 sk = sky_color(bn.d, P.sun);
+        c = make_float3(sk.x * m[0], sk.y * m[1], sk.z * m[2]);
+    } else {
+        const float3 col = color_of(P.mat_color[h.info & MAT_MASK]);
+        const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
+        const int32_t sg = (h.info & NEG_BIT) ? -1 : 1;  // the ray's step on the hit axis
+        const float l = (ax == 0u ? P.sun[0] : (ax == 1u ? P.sun[1] : P.sun[2])) * (float)(-sg);
+        const bool facing = l > 0.0f;
+        const float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
+        c = make_float3(col.x * inten * m[0], col.y * inten * m[1], col.z * inten * m[2]);
+        bool dark = false;
+        if (bn.n == 0) {
+            if (!facing) {
+                dark = true;
+            } else {
+                // shadow ray towards the sun from the centre of lastPos, through empty and liquid
+                const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
+                                     (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
+                // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
+                dark = (trace<false, false, true, false, DIRS>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
+                            .info & HIT_BIT) != 0u;
+            }
+        }
+        if (dark) c = make_float3(col.x * 0.3f * m[0], col.y * 0.3f * m[1], col.z * 0.3f * m[2]);
+    }
+    P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// Frame mode: the pixel of this lane of launch block blk (its ray o, d and record index out; out = -1 for lanes past the
+// frame's edge).  8-pixel tile rows, one wavefront per 2^(6-lh) x 2^lh footprint; frames interleave wave by wave (every
+// frame's long top rows first); the frame and tile indices are wave-uniform: their divisions run on the scalar unit.
+__device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, float o[3], float d[3], int64_t& out, uint32_t& frm,
+                                            int32_t* pxy = nullptr) {
+    const uint32_t wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
+    frm = fr;
+    const int32_t lane = (int32_t)(threadIdx.x & 63u);
+    const uint32_t tq = tile / (uint32_t)P.tiles_x;
+    int32_t trl = (int32_t)tq;
+    // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
+    // them first keeps the long tiles out of the launch's tail)
+    if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
+    const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
+    const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
+    // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
+    // sub-rows of one column of footprints are adjacent waves
+    const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
+    const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
+    const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
+    if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+        raygen_pixel(P.rg, px, py, d);
+        o[0] = P.frame_org[3 * fr + 0];
+        o[1] = P.frame_org[3 * fr + 1];
+        o[2] = P.frame_org[3 * fr + 2];
+        out = (int64_t)fr * P.frame_records + ((int64_t)trl * 8 + rr) * P.width + px;
+        if (pxy) {
+            pxy[0] = px;
+            pxy[1] = py;
+        }
+    }
+}
+
 template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
 // ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
@@ -1391,33 +1479,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
     int64_t out = -1;
     uint32_t frm = 0u;  // the wave's frame (frame mode)
     if (P.mode == MODE_FRAME) {
-        // 8x8 pixel tiles, one wavefront (64 lanes) per tile: tile-coherent rays share nodes.
-        // The tile index is wave-uniform: its division runs on the scalar unit.
-        // frames interleave wave by wave (every frame's long top rows first); the frame and tile
-        // indices are wave-uniform: their divisions run on the scalar unit
-        const uint32_t wv = (uint32_t)blk * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-        const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
-        frm = fr;
-        const int32_t lane = (int32_t)(threadIdx.x & 63u);
-        const uint32_t tq = tile / (uint32_t)P.tiles_x;
-        int32_t trl = (int32_t)tq;
-        // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
-        // them first keeps the long tiles out of the launch's tail)
-        if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
-        const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
-        const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
-        // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
-        // sub-rows of one column of footprints are adjacent waves
-        const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
-        const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
-        const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-        if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
-            raygen_pixel(P.rg, px, py, d);
-            o[0] = P.frame_org[3 * fr + 0];
-            o[1] = P.frame_org[3 * fr + 1];
-            o[2] = P.frame_org[3 * fr + 2];
-            out = (int64_t)fr * P.frame_records + ((int64_t)trl * 8 + rr) * P.width + px;
-        }
+        frame_pixel(P, blk, o, d, out, frm);
     } else if (P.mode == MODE_EXPLICIT) {
         if (g < P.n_rays) {
             d[0] = P.rdir[3 * g + 0];
@@ -1446,52 +1508,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
         const Hit h = trace<STATS, true, true, SEG, 0, false, 2>(
             P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
             &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
-        if (P.pos) {
-            reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
-            P.t[out] = h.t;
-            P.info[out] = h.info;
-        }
-        const bool hit = (h.info & HIT_BIT) != 0u;
-        const float* m = bn.m;  // finalColorMod
-        float3 c;
-        int32_t lk[3] = {P.look[0], P.look[1], P.look[2]};
-        bool lv = P.look_valid != 0;
-        if (P.look_dev) {  // (uniform: the pick ray's record, written on this stream before the launch)
-            lk[0] = P.look_dev[0];
-            lk[1] = P.look_dev[1];
-            lk[2] = P.look_dev[2];
-            lv = true;
-        }
-        if (lv && h.x == lk[0] && h.y == lk[1] && h.z == lk[2]) {
-            const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
-            c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
-        } else if (!hit) {
-            const float3 sk = sky_color(bn.d, P.sun);
-            c = make_float3(sk.x * m[0], sk.y * m[1], sk.z * m[2]);
-        } else {
-            const float3 col = color_of(P.mat_color[h.info & MAT_MASK]);
-            const uint32_t ax = (h.info >> AXIS_SHIFT) & 3u;
-            const int32_t sg = (h.info & NEG_BIT) ? -1 : 1;  // the ray's step on the hit axis
-            const float l = (ax == 0u ? P.sun[0] : (ax == 1u ? P.sun[1] : P.sun[2])) * (float)(-sg);
-            const bool facing = l > 0.0f;
-            const float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
-            c = make_float3(col.x * inten * m[0], col.y * inten * m[1], col.z * inten * m[2]);
-            bool dark = false;
-            if (bn.n == 0) {
-                if (!facing) {
-                    dark = true;
-                } else {
-                    // shadow ray towards the sun from the centre of lastPos, through empty and liquid
-                    const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
-                                         (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                    // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
-                    dark = (trace<false, false, true, false, DIRS>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
-                                .info & HIT_BIT) != 0u;
-                }
-            }
-            if (dark) c = make_float3(col.x * 0.3f * m[0], col.y * 0.3f * m[1], col.z * 0.3f * m[2]);
-        }
-        P.rgba[out] = make_float4(c.x, c.y, c.z, 0.0f);
+        shade_out<DIRS>(P, smem, path, h, bn, out);
     } else if (out >= 0) {
         Parent pfin;
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO, 1>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
