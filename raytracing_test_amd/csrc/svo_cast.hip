@@ -105,7 +105,7 @@ constexpr int kBlock = 64;    // threads per block: one wavefront per tile footp
 // were resolved to their measured winners and removed from the source; the losing sides are in git history
 // (DESIGN.md cites the commits) and build_variant.py --rev rebuilds them.  The critical-path diagnostics
 // (an iteration cap, dropping the top tile rows) are patches: tools/variants/*.patch, build_variant.py --patch)
-constexpr int kShadeWaves = 8;  // waves per SIMD the shading instances are held to (7 fits them without spills: 4 % slower)
+constexpr int kShadeWaves = 5;  // waves per SIMD of the shading instances: 88 VGPRs, no spills (its LDS — path + bounce state — allows 5-6; 6 waves: 80 VGPRs, 1.3 % slower; 8 with the bounce state in registers spilled 22 VGPRs: 2.5 % slower)
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -1455,8 +1455,8 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
 
 template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
-// ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instance runs 8 waves
-// with a 12-byte spill (2.9 % faster than 6 waves)
+// ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instances run 5 waves
+// without spills (kShadeWaves)
 __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
@@ -1470,6 +1470,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
     const Path path = {path_words + threadIdx.x};
     // hemisphere AO sample set, broadcast from LDS
     __shared__ float ao_tab[3 * 64];
+    __shared__ Bounce shade_bn[SHADE ? kBlock : 1];  // shading: the rays' bounce state (k_cast SHADE below)
     if (AO)
         for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
     __syncthreads();
@@ -1504,7 +1505,10 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
         out = 0;
     }
     if (SHADE && out >= 0) {
-        Bounce bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
+        // the ray's bounce state lives in LDS: the trace touches it only at reflections / refractions, and in registers
+        // it cost the loop spills (22 VGPRs at 8 waves; 0.4748 -> 0.4660 ms per shaded C3 frame at 5 waves without them)
+        Bounce& bn = shade_bn[threadIdx.x];
+        bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
         const Hit h = trace<STATS, true, true, SEG, 0, false, 2>(
             P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
             &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
