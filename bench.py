@@ -385,6 +385,10 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="c3: depth-12 / 1080p (the metric); c5: depth-14 / 4K; c2: the reference world / 1080p / S=300 from the "
                          "C3 pose, c2cam0 from the reference's default camera; c1: the dense 256^3 grid, 256^2 rays")
+    ap.add_argument("--inflight", type=int, choices=(1, 2), default=1,
+                    help="2: consecutive steps' casts alternate between two streams, so two frames are in flight on every rank "
+                         "(the next frame's long far-field waves fill this one's tail; a small shard of a strong-scaled frame "
+                         "gains most); the line's launch times are then each launch's own, overlapped")
     ap.add_argument("--frames", type=int, default=None,
                     help="frames per step over all GPUs (strong scaling; default: one per GPU, weak scaling)")
     ap.add_argument("--ao", type=int, default=0, help="config C4: hemisphere AO rays per primary hit (16 or 20)")
@@ -512,16 +516,17 @@ def main():
         xmode = "torch" if (args.shade or args.exchange == "torch" or args.dist_backend != "nccl") else "capi"
     gdev = torch.device("cuda", dev)
     pipe_steps = args.steps if args.pipelined_steps is None else args.pipelined_steps
-    if gather or world > 1:
+    if gather or world > 1 or args.inflight > 1:
         pipe_steps = 0  # (an N = 1 measurement beside the contract's own)
-    nbuf = 2 if (gather or pipe_steps) else 1  # the exchange (or the next launch) of step k overlaps step k+1
+    nbuf = 2 if (gather or pipe_steps or args.inflight > 1) else 1  # the exchange (or the next launch) of step k overlaps step k+1
     outs = []
     for _ in range(nbuf):
         views = rt.Tree.alloc_hits(rays_per_launch, dev, ao=args.ao > 0)
         if args.shade:
             views["rgba"] = torch.zeros((rays_per_launch, 4), dtype=torch.float32, device=gdev)
         outs.append(views)
-    cstreams = [torch.cuda.Stream(device=dev) for _ in range(2 if pipe_steps else 1)]
+    cstreams = [torch.cuda.Stream(device=dev) for _ in range(2 if (pipe_steps or args.inflight > 1) else 1)]
+    inflight = args.inflight > 1  # the timed steps alternate between the two cast streams (two frames in flight)
     stream = cstreams[0]
     xstream = torch.cuda.Stream(device=dev) if gather else None
     exch = None
@@ -597,8 +602,8 @@ def main():
             tx.drain(stream)
 
     step_no = 0
-    for _ in range(args.warmup):
-        one_step(step_no)
+    for _ in range(max(args.warmup, 2) if inflight else args.warmup):
+        one_step(step_no, pipe=inflight)
         step_no += 1
     drain()
     torch.cuda.synchronize()
@@ -609,12 +614,12 @@ def main():
     reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     # back-to-back launches on one stream: one event pair around the timed region gives their average
     # (gaps included); with an exchange in between, pairs around each launch
-    region_events = not gather and not args.launch_events
+    region_events = not gather and not args.launch_events and not inflight
     t0 = time.perf_counter()
     if region_events:
         reg[0].record(stream)
     for k in range(args.steps):
-        one_step(step_no, None if region_events else evs[k])
+        one_step(step_no, None if region_events else evs[k], pipe=inflight)
         step_no += 1
     if region_events:
         reg[1].record(stream)
@@ -721,7 +726,7 @@ def main():
         "config": {"workload": work + cfg["label"] + " primary rays per frame, camera (%g,%g,%g)->normalize(%g,%g,%g), S=%d, "
                                                      "castRayFromCam semantics" % (cfg["origin"] + cfg["cam"] + (STEPS,)),
                    "ao_samples": args.ao, "shade": args.shade, "frames_per_step": nframes, "rays_per_step": W * H * nframes,
-                   "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "gather": gather,
+                   "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "frames_in_flight": args.inflight, "gather": gather,
                    "dispatch_order": "top tile rows first",
                    "exchange": None if not gather else (
                        ("svo_cast_wire + svo_exchange_wire (C ABI, RCCL send/recv group): %d-B wire records written by the cast "
@@ -738,7 +743,8 @@ def main():
         **({"gather_verified": verified} if verified is not None else {}),
         **({"pipelined": pipelined} if pipelined is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
-                         "included)" if region_events else "a HIP event pair around every launch on its stream",
+                         "included)" if region_events else ("a HIP event pair around every launch on its stream" +
+                                                            (" (two frames in flight: overlapped launches)" if inflight else "")),
     }
     print(json.dumps(line), flush=True)
     if world > 1:

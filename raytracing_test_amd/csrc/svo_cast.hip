@@ -1410,7 +1410,7 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
                 const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                      (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
                 // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
-                dark = (trace<false, false, true, false, DIRS>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
+                dark = (trace<false, false, true, false, DIRS, false, 1>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                             .info & HIT_BIT) != 0u;
             }
         }

@@ -44,6 +44,14 @@ def test_strong_two_frames_verified():
     assert d["gather_verified"] is True, d
 
 
+def test_strong_frames_in_flight_verified():
+    """--inflight 2: consecutive steps' casts alternate between two streams (two frames in flight per rank), each
+    buffer set's exchange ordered after its own cast — every displayed frame still verifies"""
+    d = _run(29614, "--frames", "1", "--inflight", "2", "--steps", "4")
+    assert d["scaling"] == "strong" and d["config"]["frames_in_flight"] == 2
+    assert d["gather_verified"] is True, d
+
+
 def test_launcher_free_two_ranks_verified():
     """`python bench.py --gpus 2` with no launcher: bench.py starts the two ranks itself (before any GPU call),
     and the line reports the communicator's size"""
