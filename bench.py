@@ -548,6 +548,16 @@ def main():
                 raise RuntimeError("svo_exchange_info reports rank/size %s, expected (%d, %d)" % (exch.info(), rank, world))
         except rt.SvoError as e:  # keep the scaling run alive; say so on the line
             xmode, xnote = "torch", "svo_exchange_create failed (%s); torch.distributed all_to_all used" % e
+        if world > 1:
+            # every rank takes the same path: a rank whose exchange failed would otherwise wait in all_to_all while the
+            # others wait in RCCL send / recv
+            ok = torch.tensor([1 if exch is not None else 0], dtype=torch.int32, device=gdev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+            if int(ok.item()) == 0 and exch is not None:
+                torch.cuda.synchronize()
+                exch.close()
+                exch = None
+                xmode, xnote = "torch", "svo_exchange_create failed on another rank; torch.distributed all_to_all used"
         if exch is not None and n_own:
             frames_out = rt.Tree.alloc_hits(n_own * W * H, dev, ao=args.ao > 0)
     # the C-ABI exchange casts straight into wire records (svo_cast_wire: 8 B per ray from integral camera
