@@ -119,3 +119,19 @@ def test_oracle_sky_matches_numpy_restatement(oracle_mod):
         want = np.array([(f(0.2) + h3) * modifier + sv, (f(0.4) + h3) * modifier + sv, (f(1.0) + h3) * modifier], f)
         assert np.allclose(rgba[k, :3], want, rtol=0, atol=2e-6), (k, rgba[k], want)
         assert rgba[k, 3] == 0.0
+
+
+def test_shade_entries_restate_the_primary_model(oracle_mod):
+    """orc_shade_entries (the shading pass's §8(d) entries, oracle/bray.py C3_shade) rides along the shading walk with
+    the primary model's restart rule: with no shadow rays and no reflecting / refracting block in reach (a 512^2
+    terrain without water: liquid mode off, terrain has none of flags 3 / 5) it counts exactly orc_frame_entries,
+    and shadow rays only add entries and one root read each."""
+    O = oracle_mod
+    t = O.Tree.terrain(5, 512, 512)
+    org, cam = (4.0, 90.0, 4.0), O.normalize((1.0, -0.45, 1.0))
+    sun = O.normalize((2.0, 1.0, 4.0))
+    W, H = 160, 90
+    e0, _, lk0 = t.shade_entries(org, cam, W, H, 2000, sun, shadow_steps=0)
+    assert e0 == t.frame_entries(org, cam, W, H, 2000)
+    e1, sh1, lk1 = t.shade_entries(org, cam, W, H, 2000, sun, shadow_steps=75)
+    assert sh1 > 0 and e1 >= e0 and lk1 > lk0

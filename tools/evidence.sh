@@ -27,6 +27,8 @@ d g2_strong 2 29542 --steps 4 --warmup 1 --frames 1 --verify
 d g3_f2 3 29543 --steps 4 --warmup 1 --frames 2 --verify
 d g2_ao 2 29544 --steps 4 --warmup 1 --ao 16 --verify
 d g2_shade 2 29545 --steps 4 --warmup 1 --shade
+d g2_strong_if2 2 29546 --steps 4 --warmup 1 --frames 1 --inflight 2 --verify
+b c5_if2 --config c5 --frames 1 --inflight 2 --no-cpu-baseline
 step rocprof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof.json 2> $OUT/prof.err
 step rocprof_c5 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- python3 bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_c5.json 2> $OUT/prof_c5.err
 step rocprof_c4 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c4 -o run -- python3 bench.py --ao 16 --steps 10 --warmup 2 --no-cpu-baseline --pipelined-steps 0 > $OUT/bench_prof_c4.json 2> $OUT/prof_c4.err
