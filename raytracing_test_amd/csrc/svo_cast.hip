@@ -1454,10 +1454,11 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
 }
 
 template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0>
-// primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO / diagnostics instances need
-// ~80 (6 waves: AO at 8 waves spills and measured 1.7 % slower); the shading instances run 5 waves
-// without spills (kShadeWaves)
-__global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
+// primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO instances run 8 waves too (4 spilled VGPRs; with
+// the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
+// against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 5 waves without
+// spills (kShadeWaves)
+__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1468,12 +1469,8 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
     // last descent), [depth][lane]
     __shared__ uint32_t path_words[(kMaxLevels - 1) * 3 * kBlock];
     const Path path = {path_words + threadIdx.x};
-    // hemisphere AO sample set, broadcast from LDS
-    __shared__ float ao_tab[3 * 64];
+    // (the hemisphere AO sample set is read from the kernel arguments: uniform loads, no LDS)
     __shared__ Bounce shade_bn[SHADE ? kBlock : 1];  // shading: the rays' bounce state (k_cast SHADE below)
-    if (AO)
-        for (int32_t i = threadIdx.x; i < 3 * P.ao_n; i += kBlock) ao_tab[i] = P.ao_tab[i];
-    __syncthreads();
     int64_t blk = blockIdx.x;
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
@@ -1539,7 +1536,7 @@ __global__ __launch_bounds__(kBlock, (AO || STATS) ? 6 : (SHADE ? kShadeWaves : 
                 } else {
                 const float ao_o[3] = {(float)lx + 0.5f, (float)ly + 0.5f, (float)lz + 0.5f};
                 for (int32_t i = 0; i < P.ao_n; i++) {
-                    const float hv[3] = {ao_tab[3 * i], ao_tab[3 * i + 1], ao_tab[3 * i + 2]};
+                    const float hv[3] = {P.ao_tab[3 * i], P.ao_tab[3 * i + 1], P.ao_tab[3 * i + 2]};
                     float ad[3];
                     ao_dir(hv, ax, -st, ad);
                     const Hit a = trace<false>(P, mem, P.mats, path, ao_o, ad, P.ao_steps);
