@@ -43,13 +43,19 @@ struct WireParams {
     uint8_t* ao_out;
 };
 
+// the frame of frame record i: 32-bit division (a launch holds fewer than 2^32 records: wire_params; a 64-bit
+// division is a long instruction sequence on the GPU, and the decode ran two of them per record)
+__device__ __forceinline__ uint32_t wire_frame(const WireParams& Q, int64_t i) {
+    return (uint32_t)i / (uint32_t)Q.frame_records;
+}
+
 // the origin record i's ray started from
 __device__ __forceinline__ void wire_origin(const WireParams& Q, int64_t i, float o[3]) {
     if (Q.explicit_mode && Q.rorg) {
 #pragma unroll
         for (int k = 0; k < 3; k++) o[k] = Q.rorg[3 * i + k];
     } else {
-        const int64_t f = Q.explicit_mode ? 0 : i / Q.frame_records;
+        const uint32_t f = Q.explicit_mode ? 0u : wire_frame(Q, i);
 #pragma unroll
         for (int k = 0; k < 3; k++) o[k] = Q.frame_org[3 * f + k];
     }
@@ -57,11 +63,12 @@ __device__ __forceinline__ void wire_origin(const WireParams& Q, int64_t i, floa
 
 // frame and pixel of frame record i (svo_cast_rays' record order over the shard's tile rows)
 __device__ __forceinline__ void wire_pixel(const WireParams& Q, int64_t i, int64_t& f, int32_t& px, int32_t& py) {
-    f = i / Q.frame_records;
-    const int64_t j = i - f * Q.frame_records;
-    const int64_t lr = j / Q.width;
-    px = (int32_t)(j - lr * Q.width);
-    py = (int32_t)(((int64_t)Q.tile_row_start + (lr >> 3) * Q.tile_row_step) * 8 + (lr & 7));
+    const uint32_t fu = wire_frame(Q, i);
+    f = fu;
+    const uint32_t j = (uint32_t)i - fu * (uint32_t)Q.frame_records;
+    const uint32_t lr = j / (uint32_t)Q.width;
+    px = (int32_t)(j - lr * (uint32_t)Q.width);
+    py = (int32_t)(((int64_t)Q.tile_row_start + (int64_t)(lr >> 3) * Q.tile_row_step) * 8 + (lr & 7u));
 }
 
 // one record from a ray's result (its origin o): 8 or 12 B at wire record i
@@ -87,13 +94,16 @@ __device__ __forceinline__ void wire_put(uint32_t* wire, bool compact, int64_t i
 // record i back into a hit record (at record i, or at its pixel of the whole frames with Q.scatter)
 __device__ __forceinline__ void wire_get(const WireParams& Q, int64_t i) {
     float o[3];
-    wire_origin(Q, i, o);
     int64_t out = i;
     int32_t px = 0, py = 0;
     if (!Q.explicit_mode) {
         int64_t f;
         wire_pixel(Q, i, f, px, py);
+#pragma unroll
+        for (int k = 0; k < 3; k++) o[k] = Q.frame_org[3 * f + k];
         if (Q.scatter) out = f * Q.frame_pixels + (int64_t)py * Q.width + px;
+    } else {
+        wire_origin(Q, i, o);
     }
     int4 ps;
     float t;
