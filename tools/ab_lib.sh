@@ -16,7 +16,8 @@ import json, sys, glob, statistics, os
 tag = sys.argv[1]
 for L in sys.argv[2:]:
     n = os.path.basename(L)[:-3] if L.endswith('.so') else L
-    ds = [json.load(open(f)) for f in sorted(glob.glob('gpurun_out/%s/ab_%s_*.json' % (tag, n)))]
+    # (the last JSON line: an RCCL exchange prints its banner to stdout first)
+    ds = [json.loads([l for l in open(f) if l.startswith('{')][-1]) for f in sorted(glob.glob('gpurun_out/%s/ab_%s_*.json' % (tag, n)))]
     ms = [d['roofline']['avg_launch_ms'] if d.get('roofline') else d['ms_per_step'] for d in ds]  # (shaded: no roofline)
     print('lib=%-22s ms min %.4f median %.4f  (%s)' % (n, min(ms), statistics.median(ms), ' '.join('%.4f' % m for m in ms)))
 PY
