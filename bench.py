@@ -518,7 +518,10 @@ def main():
     pipe_steps = args.steps if args.pipelined_steps is None else args.pipelined_steps
     if gather or world > 1 or args.inflight > 1:
         pipe_steps = 0  # (an N = 1 measurement beside the contract's own)
-    nbuf = 2 if (gather or pipe_steps or args.inflight > 1) else 1  # the exchange (or the next launch) of step k overlaps step k+1
+    # the exchange (or the next launch) of step k overlaps step k+1.  With an exchange, three buffer sets: step k's
+    # decode runs beside cast k+1 and gets wave slots only in that cast's tail, so cast k+2 reusing step k's buffers would
+    # wait for it (a bubble every step: the 1-rank exchange's k_wire_scatter spans 150 us of the 173-us cast beside it)
+    nbuf = 3 if gather else (2 if (pipe_steps or args.inflight > 1) else 1)
     outs = []
     for _ in range(nbuf):
         views = rt.Tree.alloc_hits(rays_per_launch, dev, ao=args.ao > 0)
@@ -622,16 +625,25 @@ def main():
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps)]
     reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-    # back-to-back launches on one stream: one event pair around the timed region gives their average
-    # (gaps included); with an exchange in between, pairs around each launch
-    region_events = not gather and not args.launch_events and not inflight
+    # one event pair around the timed region on the cast stream gives the average launch (gaps and the waits for the
+    # exchange included); timing events around every launch (--launch-events) would serialise the cast and exchange
+    # streams (1-rank exchange: 0.197 ms per step with them, ~0.175 without — tools/xchg_host.py)
+    # (two frames in flight: the pair spans both cast streams — the second waits for the opening event, the first for the
+    # second's last launch before the closing one)
+    region_events = not args.launch_events
     t0 = time.perf_counter()
     if region_events:
         reg[0].record(stream)
+        if inflight:
+            cstreams[1].wait_event(reg[0])
     for k in range(args.steps):
         one_step(step_no, None if region_events else evs[k], pipe=inflight)
         step_no += 1
     if region_events:
+        if inflight:
+            j = torch.cuda.Event()
+            j.record(cstreams[1])
+            stream.wait_event(j)
         reg[1].record(stream)
     drain()
     torch.cuda.synchronize()
@@ -753,8 +765,8 @@ def main():
         **({"gather_verified": verified} if verified is not None else {}),
         **({"pipelined": pipelined} if pipelined is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
-                         "included)" if region_events else ("a HIP event pair around every launch on its stream" +
-                                                            (" (two frames in flight: overlapped launches)" if inflight else "")),
+                         "included" + ("; two frames in flight: the pair spans both cast streams" if inflight else "") + ")"
+                         if region_events else "a HIP event pair around every launch on its stream (--launch-events)",
     }
     print(json.dumps(line), flush=True)
     if world > 1:
