@@ -91,9 +91,12 @@ Rccl& rccl() {
         if (r_ != ncclSuccess) SVO_FAIL(SVO_EDEVICE, std::string(#expr " failed: ") + rccl().GetErrorString(r_)); \
     } while (0)
 
-// One source shard's wire records (and AO counts) -> their pixels of the whole frames (svo_wire.h)
-__global__ __launch_bounds__(256) void k_wire_scatter(const WireParams Q) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// One source shard's wire records (and AO counts) -> their pixels of the whole frames (svo_wire.h).  1024-thread blocks:
+// the decode runs beside the next step's cast, whose one-wave blocks hold every wave slot until its tail; a 16-wave block
+// starts only where a CU has emptied, i.e. in that tail (forced 1-rank exchange at C3: 0.1844 -> 0.1822 ms per step
+// against 256-thread blocks; 64-thread blocks, which take slots as soon as single cast waves retire: 0.1900)
+__global__ __launch_bounds__(1024) void k_wire_scatter(const WireParams Q) {
+    const int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
     if (i >= Q.n) return;
     wire_get(Q, i);
 }
@@ -271,7 +274,7 @@ static int exchange_wire(svo_exchange* x, const svo_tree* t, const svo_cast_desc
             Q.t = frames_out->t + (size_t)(k * frame);
             Q.info = frames_out->info + (size_t)(k * frame);
             Q.ao_out = ao ? frames_out->ao + (size_t)(k * frame) : nullptr;
-            hipLaunchKernelGGL(k_wire_scatter, dim3((uint32_t)((Q.n + 255) / 256)), dim3(256), 0, st, Q);
+            hipLaunchKernelGGL(k_wire_scatter, dim3((uint32_t)((Q.n + 1024 - 1) / 1024)), dim3(1024), 0, st, Q);
             HIP_TRY(hipGetLastError(), SVO_EDEVICE);
         }
     }
