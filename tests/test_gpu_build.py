@@ -33,6 +33,12 @@ def test_terrain_gpu_equals_host(rt, torch_cuda, levels, W, L, view):
     g, h = rt.Tree.terrain_gpu(levels, W, L, 0, view=view), rt.Tree.terrain(levels, W, L, view=view)
     assert g.info().view == view
     _same(g, h, "terrain L%d %dx%d view %d" % (levels, W, L, view))
+    # the column-ceiling tables the casts read (ceilings, pairs, per-level quads) are the same for both builders
+    h.upload(0)
+    lg, cg, pg = g.device_ceilings()
+    lh, ch, ph = h.device_ceilings()
+    assert lg == lh and np.array_equal(cg, ch) and np.array_equal(pg, ph)
+    assert np.array_equal(g.device_ceiling_quads(), h.device_ceiling_quads())
 
 
 def test_heightfield_gpu_equals_host(rt, torch_cuda):
