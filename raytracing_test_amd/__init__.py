@@ -42,6 +42,9 @@ CAST_WIDE_ADDR = 2048  # 64-bit node addresses even for trees below 2^28 nodes (
 CAST_SEGMENTS = 4096  # force the kernel instance with segment-exact crossings (results identical)
 CAST_NO_OCTANT = 16384  # per-wave step-sign flags instead of the launch's compiled-in sign octant (results identical)
 CAST_NO_CEILINGS = 32768  # walk the tree instead of crossing column-ceiling boxes (results identical)
+CAST_NO_SCHEDULE = 65536  # keep the default dispatch order instead of the last frame's longest-first schedule (results identical)
+SCHED_MIN_BLOCKS = 4096  # frames of more blocks are scheduled (SVO_SCHED_MIN_BLOCKS)
+SCHED_PRIMARY, SCHED_AO, SCHED_SHADE = 0, 1, 2  # Tree.schedule kinds
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
@@ -141,7 +144,7 @@ ABI_SYMBOLS = (
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
-    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_cast_ray_from_cam_async",
+    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_tree_schedule", "svo_cast_ray_from_cam_async",
 )
 
 
@@ -185,6 +188,7 @@ def lib():
                      ("svo_tree_guard_trips", [vp, C.POINTER(C.c_uint64), i32]),
                      ("svo_tree_device_ceilings", [vp, vp, vp, C.c_int64, C.POINTER(i32), C.POINTER(C.c_int64)]),
                      ("svo_tree_device_ceiling_quads", [vp, vp, C.c_int64, C.POINTER(C.c_int64)]),
+                     ("svo_tree_schedule", [vp, vp, C.c_int32, vp, vp, C.c_int64, C.POINTER(C.c_int64)]),
                      ("svo_cast_ray_from_cam_async", [vp, f3, f3, i32, vp, vp])):
         if hasattr(L, name):
             getattr(L, name).argtypes = at
@@ -662,6 +666,20 @@ class Tree:
         _check(lib().svo_tree_device_ceiling_quads(self._h, q.ctypes.data_as(C.c_void_p), n.value, C.byref(n)),
                "svo_tree_device_ceiling_quads")
         return q
+
+    def schedule(self, kind=0, stream=None):
+        """(order, cost) of the frame schedule of (stream, kind: SCHED_PRIMARY / SCHED_AO / SCHED_SHADE) (svo_tree_schedule):
+        the next frame's dispatch order (slot -> frame block) and the last frame's block durations (100 MHz ticks);
+        (None, None) before a scheduled frame"""
+        s = getattr(stream, "cuda_stream", stream)
+        n = C.c_int64()
+        _check(lib().svo_tree_schedule(self._h, C.c_void_p(s) if s else None, kind, None, None, 0, C.byref(n)), "svo_tree_schedule")
+        if n.value == 0:
+            return None, None
+        o, c = np.zeros(n.value, np.uint32), np.zeros(n.value, np.uint32)
+        _check(lib().svo_tree_schedule(self._h, C.c_void_p(s) if s else None, kind, o.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+                                       n.value, C.byref(n)), "svo_tree_schedule")
+        return o, c
 
     def guard_trips(self, reset=False):
         """Rays of launches over this tree that ended on the progress guard (svo_tree_guard_trips): 0 unless a

@@ -92,6 +92,21 @@ struct svo_tree {
     std::vector<uint32_t> ceilp_host;
     // column rectangles {x0, z0, x1, z1} (wrapped, half-open) whose ceilings svo_tree_update's edits may have changed
     std::vector<std::array<int64_t, 4>> ceil_dirty;
+    // frame schedules (svo_cast.hip sched_attach): per (stream, launch kind) the block durations of the last frame of one
+    // geometry and the dispatch order sorted from them (longest first) for the next; d_buf = u32 order[blocks], u32
+    // cost[blocks], u8 key[blocks]
+    struct Sched {
+        void* stream;
+        int32_t kind;
+        int64_t sig[7];
+        int64_t blocks;
+        void* d_buf;
+        uint64_t last_use;
+        bool primed;  // order holds a sorted schedule (else: the frame runs in the natural order and writes costs)
+    };
+    mutable std::vector<Sched> scheds;
+    mutable std::mutex sched_mu;
+    mutable uint64_t sched_clock = 0;
 };
 
 namespace svo {
