@@ -1467,7 +1467,9 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
     // diagnostics: block start / end stamps (100 MHz s_memrealtime) after the 16 counters
-    const unsigned long long t_start = (STAMPS || P.sched_cost) ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    // (frame schedules: shading instances only — sched_attach; the primary instances compile without the hooks)
+    const bool sched = SHADE && P.sched_cost;
+    const unsigned long long t_start = (STAMPS || sched) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // per-lane node path (mask and first-child index of the interior node at each depth of the
     // last descent), [depth][lane]
     __shared__ uint32_t path_words[(kMaxLevels - 1) * 3 * kBlock];
@@ -1475,7 +1477,7 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
     // (the hemisphere AO sample set is read from the kernel arguments: uniform loads, no LDS)
     __shared__ Bounce shade_bn[SHADE ? kBlock : 1];  // shading: the rays' bounce state (k_cast SHADE below)
     int64_t blk = blockIdx.x;
-    if (P.sched_order) blk = P.sched_order[blockIdx.x];  // (frame mode: the schedule's block at this dispatch slot)
+    if (SHADE && P.sched_order) blk = P.sched_order[blockIdx.x];  // (frame mode: the schedule's block at this dispatch slot)
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
@@ -1551,14 +1553,14 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
             P.ao[out] = (uint8_t)cnt;
         }
     }
-    if (STAMPS || P.sched_cost) {
+    if (STAMPS || sched) {
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();  // (one wavefront per block: every lane is done)
         if (threadIdx.x == 0) {
             if (STAMPS) {
                 P.stats[SVO_STATS_HEADER + 2 * blockIdx.x] = t_start;
                 P.stats[SVO_STATS_HEADER + 2 * blockIdx.x + 1] = t_end;
             }
-            if (P.sched_cost) P.sched_cost[blk] = (uint32_t)std::min(t_end - t_start, 0xFFFFFFFFull);
+            if (sched) P.sched_cost[blk] = (uint32_t)std::min(t_end - t_start, 0xFFFFFFFFull);
         }
     }
 }
