@@ -45,6 +45,7 @@ CAST_NO_CEILINGS = 32768  # walk the tree instead of crossing column-ceiling box
 CAST_NO_SCHEDULE = 65536  # keep the default dispatch order instead of the last frame's longest-first schedule (results identical)
 SCHED_MIN_BLOCKS = 4096  # frames of more blocks are scheduled (SVO_SCHED_MIN_BLOCKS)
 SCHED_PRIMARY, SCHED_AO, SCHED_SHADE = 0, 1, 2  # Tree.schedule kinds
+SCHED_GROUP = 4  # the schedule orders groups of this many consecutive blocks (SVO_SCHED_GROUP)
 STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "brick_steps", "plain_steps", "lane_work",
               "wave_max_work_x64", "skips_4", "skips_16", "skips_64", "skips_256plus", "bricks",
               "wave_iters", "wave_brick_steps",
@@ -669,14 +670,15 @@ class Tree:
 
     def schedule(self, kind=0, stream=None):
         """(order, cost) of the frame schedule of (stream, kind: SCHED_PRIMARY / SCHED_AO / SCHED_SHADE) (svo_tree_schedule):
-        the next frame's dispatch order (slot -> frame block) and the last frame's block durations (100 MHz ticks);
+        the next frame's dispatch order of groups of SCHED_GROUP blocks (slot group -> frame group) and the last frame's
+        block durations (100 MHz ticks);
         (None, None) before a scheduled frame"""
         s = getattr(stream, "cuda_stream", stream)
         n = C.c_int64()
         _check(lib().svo_tree_schedule(self._h, C.c_void_p(s) if s else None, kind, None, None, 0, C.byref(n)), "svo_tree_schedule")
         if n.value == 0:
             return None, None
-        o, c = np.zeros(n.value, np.uint32), np.zeros(n.value, np.uint32)
+        o, c = np.zeros(n.value // SCHED_GROUP, np.uint32), np.zeros(n.value, np.uint32)
         _check(lib().svo_tree_schedule(self._h, C.c_void_p(s) if s else None, kind, o.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
                                        n.value, C.byref(n)), "svo_tree_schedule")
         return o, c

@@ -105,6 +105,7 @@ struct CastParams {
 };
 
 constexpr int kBlock = 64;    // threads per block: one wavefront per tile footprint
+constexpr int kSchedGroup = SVO_SCHED_GROUP;  // frame schedules order groups of this many consecutive blocks (sched_attach)
 // (round 3's A/B switches — ceiling caching and packing, wave-gated boxes, XCD grouping, issue priority —
 // were resolved to their measured winners and removed from the source; the losing sides are in git history
 // (DESIGN.md cites the commits) and build_variant.py --rev rebuilds them.  The critical-path diagnostics
@@ -1477,7 +1478,8 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
     // (the hemisphere AO sample set is read from the kernel arguments: uniform loads, no LDS)
     __shared__ Bounce shade_bn[SHADE ? kBlock : 1];  // shading: the rays' bounce state (k_cast SHADE below)
     int64_t blk = blockIdx.x;
-    if (SHADE && P.sched_order) blk = P.sched_order[blockIdx.x];  // (frame mode: the schedule's block at this dispatch slot)
+    // (frame mode: the schedule's group of kSchedGroup blocks at this dispatch slot's group)
+    if (SHADE && P.sched_order) blk = (int64_t)P.sched_order[blockIdx.x / kSchedGroup] * kSchedGroup + blockIdx.x % kSchedGroup;
     const int64_t g = blk * kBlock + threadIdx.x;
     float o[3] = {0.0f, 0.0f, 0.0f}, d[3] = {0.0f, 0.0f, 0.0f};
     int64_t out = -1;
@@ -1565,30 +1567,45 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
     }
 }
 
-// The next frame's dispatch order from this frame's block durations (one workgroup): a counting sort, longest first, on
-// 256 linear buckets of [0, max] (a bucket is max/256 wide: about 1 us of a 250 us block); blocks within a bucket in any
-// order.  Every block index lands once: the order is a permutation whatever the durations.
-constexpr int kSchedThreads = 1024, kSchedBuckets = 256;
-__global__ __launch_bounds__(kSchedThreads) void k_sched_order(const uint32_t* __restrict__ cost, uint8_t* __restrict__ key,
-                                                               uint32_t* __restrict__ order, uint32_t n) {
-    __shared__ uint32_t wmax[kSchedThreads / 64];
+// The next frame's dispatch order from this frame's block durations (one workgroup): a counting sort, longest first, of
+// groups of kSchedGroup consecutive blocks (a group's duration: its longest block's) on 256 logarithmic buckets (8 per
+// octave: durations within 12.5 % share one; groups within a bucket in any order).  Its cost is the LDS atomics, which
+// serialise on a bucket (most blocks share a few): per block 24 us for a 1080p frame, per group of 4 a quarter; the
+// groups also keep 64 x 4-pixel strips of a tile row together.  All of a thread's loads go out together (kSchedBatch
+// per thread, kept in registers for the scatter up to 32768 groups).  The key is a function of the duration alone,
+// and every group index lands once: the order is a permutation whatever the durations.
+constexpr int kSchedThreads = 1024, kSchedBuckets = 256, kSchedBatch = 32;
+__device__ __forceinline__ uint32_t sched_key(uint32_t c) {
+    // bits 20.. of the f32 value: exponent and 3 mantissa bits; c >= 1 gives 0 .. 255 from 1 to 2^32 (c near 2^32 rounds
+    // to 2^32: 256, clamped)
+    if (c == 0u) return (uint32_t)(kSchedBuckets - 1);
+    return (uint32_t)(kSchedBuckets - 1) - std::min((__float_as_uint((float)c) >> 20) - (127u << 3), (uint32_t)(kSchedBuckets - 1));
+}
+// the duration of group i: its longest block (kSchedGroup == 4: one 16-B load)
+__device__ __forceinline__ void sched_load(const uint32_t* __restrict__ cost, uint32_t n, uint32_t base, uint32_t (&c)[kSchedBatch]) {
+    static_assert(kSchedGroup == 4, "one uint4 per group");
+#pragma unroll
+    for (int j = 0; j < kSchedBatch; j++) {
+        const uint32_t i = base + (uint32_t)j * kSchedThreads + threadIdx.x;
+        const uint4 q = i < n ? reinterpret_cast<const uint4*>(cost)[i] : make_uint4(0u, 0u, 0u, 0u);
+        c[j] = std::max(std::max(q.x, q.y), std::max(q.z, q.w));
+    }
+}
+// n: groups
+__global__ __launch_bounds__(kSchedThreads) void k_sched_order(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order, uint32_t n) {
     __shared__ uint32_t hist[kSchedBuckets];
     __shared__ uint32_t wsum[kSchedBuckets / 64];
     const uint32_t tid = threadIdx.x;
-    uint32_t m = 0u;
-    for (uint32_t i = tid; i < n; i += kSchedThreads) m = std::max(m, cost[i]);
-    for (int o = 32; o > 0; o >>= 1) m = std::max(m, (uint32_t)__shfl_xor((int)m, o));
-    if ((tid & 63u) == 0u) wmax[tid >> 6] = m;
+    constexpr uint32_t kRound = (uint32_t)kSchedThreads * kSchedBatch;
+    uint32_t c[kSchedBatch];
+    sched_load(cost, n, 0u, c);
     if (tid < kSchedBuckets) hist[tid] = 0u;
     __syncthreads();
-    m = 0u;
-    for (int w = 0; w < kSchedThreads / 64; w++) m = std::max(m, wmax[w]);
-    const uint64_t scale = (uint64_t)m + 1u;
-    // (the key of block i is written and read back by the same thread: the permutation holds even if cost changed)
-    for (uint32_t i = tid; i < n; i += kSchedThreads) {
-        const uint32_t b = (uint32_t)(kSchedBuckets - 1) - (uint32_t)(((uint64_t)cost[i] * kSchedBuckets) / scale);
-        key[i] = (uint8_t)b;
-        atomicAdd(&hist[b], 1u);
+    for (uint32_t base = 0; base < n; base += kRound) {
+        if (base) sched_load(cost, n, base, c);
+#pragma unroll
+        for (int j = 0; j < kSchedBatch; j++)
+            if (base + (uint32_t)j * kSchedThreads + tid < n) atomicAdd(&hist[sched_key(c[j])], 1u);
     }
     __syncthreads();
     // exclusive scan of the histogram: per wavefront, then the wavefronts' totals
@@ -1604,12 +1621,19 @@ __global__ __launch_bounds__(kSchedThreads) void k_sched_order(const uint32_t* _
     }
     __syncthreads();
     if (tid < kSchedBuckets) {
-        uint32_t base = 0u;
-        for (uint32_t w = 0; w < (tid >> 6); w++) base += wsum[w];
-        hist[tid] = base + inc - v;
+        uint32_t b = 0u;
+        for (uint32_t w = 0; w < (tid >> 6); w++) b += wsum[w];
+        hist[tid] = b + inc - v;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < n; i += kSchedThreads) order[atomicAdd(&hist[key[i]], 1u)] = i;
+    for (uint32_t base = 0; base < n; base += kRound) {
+        if (n > kRound) sched_load(cost, n, base, c);  // (one round: the durations are still in c)
+#pragma unroll
+        for (int j = 0; j < kSchedBatch; j++) {
+            const uint32_t i = base + (uint32_t)j * kSchedThreads + tid;
+            if (i < n) order[atomicAdd(&hist[sched_key(c[j])], 1u)] = i;
+        }
+    }
 }
 
 // The AO plan of (n samples, `steps`) (see ao_count_plan): every (sample, face) ray simulated with
@@ -1909,14 +1933,21 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
 // dispatched first (top tile rows), and the sorted order loses the neighbouring tiles' shared node reads — C3 0.1678 ->
 // 0.1941 ms, C4 0.2314 -> 0.2569, C5 0.5078 -> 0.6209 when scheduled.
 constexpr size_t kSchedMax = 16;  // schedules per tree (least recently used replaced)
+// A schedule predicts a frame from the last one: a camera that turned more than kSchedTurn or moved more than kSchedMove
+// voxels since runs the default order (and re-primes).  Measured (tools/shade_motion.py, r04_ax): a still view 0.462 ->
+// 0.368 ms; 0.25 deg + 0.14 voxels per frame 0.400 -> 0.395; 2 deg per frame 0.292 -> 0.374 and a cut every frame
+// 0.308 -> 0.358 when a stale order was used — a wrong order is worse than the default one.  A frame far from the last
+// one is not sorted after either (the sort costs ~9 us): the schedule comes back one frame after the camera settles.
+constexpr float kSchedTurnCos = 0.99996f;  // cos(0.5 deg)
+constexpr float kSchedMove = 1.0f;
 struct SchedUse {  // a launch's schedule (sched_attach), by value: the tree's list may change under other threads
     uint32_t* base = nullptr;
     int64_t blocks = 0;
     int32_t kind = 0;
 };
-SchedUse sched_attach(const svo_tree* t, CastParams& P, int32_t kind, int64_t blocks, hipStream_t st) {
+SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, int32_t kind, int64_t blocks, hipStream_t st) {
     if (P.mode != MODE_FRAME || (P.flags & (SVO_CAST_NO_SCHEDULE | SVO_CAST_STATS)) || blocks <= SVO_SCHED_MIN_BLOCKS ||
-        blocks > 0x7FFFFFFFll)
+        blocks > 0x7FFFFFFFll || blocks % kSchedGroup)
         return SchedUse{};
     const int64_t sig[7] = {P.width, P.height, P.n_frames, P.tile_row_start, P.tile_row_step, P.tile_lh, (int64_t)(P.flags & SVO_CAST_BOTTOM_FIRST)};
     std::lock_guard<std::mutex> lock(t->sched_mu);
@@ -1930,7 +1961,7 @@ SchedUse sched_attach(const svo_tree* t, CastParams& P, int32_t kind, int64_t bl
             (void)hipFree(lru->d_buf);  // (synchronises the device: no launch still reads it)
             t->scheds.erase(lru);
         }
-        t->scheds.push_back(svo_tree::Sched{(void*)st, kind, {0}, 0, nullptr, 0, false});
+        t->scheds.push_back(svo_tree::Sched{(void*)st, kind, {0}, 0, nullptr, 0, false, {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}});
         s = &t->scheds.back();
     }
     s->last_use = ++t->sched_clock;
@@ -1939,7 +1970,7 @@ SchedUse sched_attach(const svo_tree* t, CastParams& P, int32_t kind, int64_t bl
             if (s->d_buf) (void)hipFree(s->d_buf);
             s->d_buf = nullptr;
             s->blocks = 0;
-            if (hipMalloc(&s->d_buf, (size_t)blocks * 9) != hipSuccess) {  // (no schedule; the launch runs unscheduled)
+            if (hipMalloc(&s->d_buf, (size_t)blocks * 8) != hipSuccess) {  // (no schedule; the launch runs unscheduled)
                 (void)hipGetLastError();
                 s->d_buf = nullptr;
                 return SchedUse{};
@@ -1949,16 +1980,24 @@ SchedUse sched_attach(const svo_tree* t, CastParams& P, int32_t kind, int64_t bl
         std::copy(sig, sig + 7, s->sig);
         s->primed = false;
     }
+    const float cam[6] = {P.frame_org[0], P.frame_org[1], P.frame_org[2], d->cam_dir[0], d->cam_dir[1], d->cam_dir[2]};
+    const float dx = cam[0] - s->cam[0], dy = cam[1] - s->cam[1], dz = cam[2] - s->cam[2];
+    const float cs = cam[3] * s->cam[3] + cam[4] * s->cam[4] + cam[5] * s->cam[5];
+    const bool near = dx * dx + dy * dy + dz * dz <= kSchedMove * kSchedMove && cs >= kSchedTurnCos;
+    std::copy(cam, cam + 6, s->cam);
     uint32_t* base = reinterpret_cast<uint32_t*>(s->d_buf);
-    P.sched_order = s->primed ? base : nullptr;
+    P.sched_order = s->primed && near ? base : nullptr;
     P.sched_cost = base + blocks;
+    if (!near) {  // (a moving camera: no sort after this frame; the first frame near it sorts for the next)
+        s->primed = false;
+        return SchedUse{nullptr, blocks, kind};
+    }
     return SchedUse{base, blocks, kind};
 }
 // after the launch of a scheduled frame: the next frame's order (the schedule counts as sorted once the sort is queued)
 int sched_order(const svo_tree* t, const SchedUse& u, hipStream_t st) {
     if (!u.base) return SVO_OK;
-    hipLaunchKernelGGL(k_sched_order, dim3(1), dim3(kSchedThreads), 0, st, u.base + u.blocks, reinterpret_cast<uint8_t*>(u.base + 2 * u.blocks),
-                       u.base, (uint32_t)u.blocks);
+    hipLaunchKernelGGL(k_sched_order, dim3(1), dim3(kSchedThreads), 0, st, u.base + u.blocks, u.base, (uint32_t)(u.blocks / kSchedGroup));
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     std::lock_guard<std::mutex> lock(t->sched_mu);
     for (auto& e : t->scheds)
@@ -2296,7 +2335,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         else if (!(P.sun[k] > 0.0f)) sun_dirs = 0;
     }
     const bool wide = wide_nodes(t, d->flags) || wide_nodes(sc, d->flags);
-    const SchedUse sch = sched_attach(t, P, 2, blocks, (hipStream_t)stream);
+    const SchedUse sch = sched_attach(t, d, P, 2, blocks, (hipStream_t)stream);
     if (P.flags & SVO_CAST_STATS) launch_cast<true, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     else if (P.flags & SVO_CAST_TIMELINE) launch_cast<false, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     else launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, sun_dirs);
@@ -2486,7 +2525,7 @@ extern "C" int svo_tree_schedule(const svo_tree* t, void* stream, int32_t kind, 
         *n = e.blocks;
         if ((order || cost) && cap < *n) SVO_FAIL(SVO_ERANGE, "svo_tree_schedule: buffer too small");
         const uint32_t* base = reinterpret_cast<const uint32_t*>(e.d_buf);
-        if (order) HIP_TRY(hipMemcpy(order, base, *n * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
+        if (order) HIP_TRY(hipMemcpy(order, base, *n / kSchedGroup * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
         if (cost) HIP_TRY(hipMemcpy(cost, base + e.blocks, *n * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
     }
     return SVO_OK;

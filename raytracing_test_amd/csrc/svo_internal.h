@@ -94,7 +94,7 @@ struct svo_tree {
     std::vector<std::array<int64_t, 4>> ceil_dirty;
     // frame schedules (svo_cast.hip sched_attach): per (stream, launch kind) the block durations of the last frame of one
     // geometry and the dispatch order sorted from them (longest first) for the next; d_buf = u32 order[blocks], u32
-    // cost[blocks], u8 key[blocks]
+    // cost[blocks]
     struct Sched {
         void* stream;
         int32_t kind;
@@ -103,6 +103,7 @@ struct svo_tree {
         void* d_buf;
         uint64_t last_use;
         bool primed;  // order holds a sorted schedule (else: the frame runs in the natural order and writes costs)
+        float cam[6];  // the camera (origin of the launch's first frame, direction) of the frame whose durations it holds
     };
     mutable std::vector<Sched> scheds;
     mutable std::mutex sched_mu;

@@ -36,10 +36,15 @@ def _shade(worlds, cam, w=W, h=H, flags=0, stream=None):
 
 
 def _check_schedule(order, cost, label):
+    assert len(cost) == len(order) * rt.SCHED_GROUP, label
+    cost = cost.reshape(-1, rt.SCHED_GROUP).max(axis=1)  # a group's duration: its longest block's
     n = len(order)
     assert np.array_equal(np.sort(order), np.arange(n, dtype=np.uint32)), label + ": order is not a permutation"
-    b = (cost.astype(np.uint64) * 256) // (np.uint64(cost.max()) + 1)
-    assert np.all(np.diff(b[order].astype(np.int64)) <= 0), label + ": not longest first"
+    # the sort's 256 logarithmic buckets (k_sched_order's sched_key: f32 exponent and 3 mantissa bits), longest first
+    k = np.minimum((cost.astype(np.float32).view(np.uint32) >> 20).astype(np.int64) - 127 * 8, 255)
+    key = np.where(cost == 0, 255, 255 - k)
+    assert np.all(np.diff(key[order]) >= 0), label + ": not longest first"
+    assert np.all(np.diff(cost[order][::max(1, n // 64)].astype(np.int64)) <= cost.max() // 7), label
     assert cost.max() > 0, label
 
 
@@ -52,14 +57,14 @@ def test_shaded_frames_identical_under_schedule(worlds, torch_cuda):
         for rep in range(2):
             assert np.array_equal(_shade(worlds, cam, stream=s), ref), "camera %d frame %d" % (i, rep)
     order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
-    assert order is not None and len(order) == solid.blocks(solid.frame_desc(ORG, rt.normalize(cams[0]), W, H, S))
+    assert order is not None and len(order) * rt.SCHED_GROUP == solid.blocks(solid.frame_desc(ORG, rt.normalize(cams[0]), W, H, S))
     _check_schedule(order, cost, "shading")
     # a new geometry starts over in the default order, then schedules
     ref = _shade(worlds, cams[0], 1280, 720, flags=rt.CAST_NO_SCHEDULE, stream=s)
     for rep in range(2):
         assert np.array_equal(_shade(worlds, cams[0], 1280, 720, stream=s), ref), "720p frame %d" % rep
     order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
-    assert len(order) == 1280 * 720 // 64
+    assert len(order) == 1280 * 720 // 64 // rt.SCHED_GROUP
     _check_schedule(order, cost, "shading 720p")
 
 
@@ -69,6 +74,11 @@ def test_small_frames_and_primary_casts_keep_no_schedule(worlds, torch_cuda):
     ref = _shade(worlds, (1.0, -0.45, 1.0), 256, 256, flags=rt.CAST_NO_SCHEDULE, stream=s)
     assert np.array_equal(_shade(worlds, (1.0, -0.45, 1.0), 256, 256, stream=s), ref)
     assert 256 * 256 // 64 <= rt.SCHED_MIN_BLOCKS
+    assert solid.schedule(rt.SCHED_SHADE, stream=s) == (None, None)
+    # 1000 x 1000: 15625 blocks, not a multiple of the schedule's groups
+    ref = _shade(worlds, (1.0, -0.45, 1.0), 1000, 1000, flags=rt.CAST_NO_SCHEDULE, stream=s)
+    for rep in range(2):
+        assert np.array_equal(_shade(worlds, (1.0, -0.45, 1.0), 1000, 1000, stream=s), ref)
     assert solid.schedule(rt.SCHED_SHADE, stream=s) == (None, None)
     for ao in (0, 16):
         solid.cast_frame(ORG, rt.normalize((1.0, -0.45, 1.0)), W, H, S, stream=s, ao_samples=ao)
