@@ -54,14 +54,14 @@ def test_shaded_frames_identical_under_schedule(worlds, torch_cuda):
     cams = [(1.0, -0.45, 1.0), (1.0, -0.43, 1.02), (0.97, -0.47, 1.0)]  # a camera turning frame to frame
     for i, cam in enumerate(cams):
         ref = _shade(worlds, cam, flags=rt.CAST_NO_SCHEDULE, stream=s)
-        for rep in range(2):
+        for rep in range(3):  # (a camera 1-2 deg from the last: default order, then sorted, then scheduled)
             assert np.array_equal(_shade(worlds, cam, stream=s), ref), "camera %d frame %d" % (i, rep)
     order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
     assert order is not None and len(order) * rt.SCHED_GROUP == solid.blocks(solid.frame_desc(ORG, rt.normalize(cams[0]), W, H, S))
     _check_schedule(order, cost, "shading")
     # a new geometry starts over in the default order, then schedules
     ref = _shade(worlds, cams[0], 1280, 720, flags=rt.CAST_NO_SCHEDULE, stream=s)
-    for rep in range(2):
+    for rep in range(3):
         assert np.array_equal(_shade(worlds, cams[0], 1280, 720, stream=s), ref), "720p frame %d" % rep
     order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
     assert len(order) == 1280 * 720 // 64 // rt.SCHED_GROUP
@@ -106,3 +106,21 @@ def test_two_streams_keep_separate_schedules(worlds, torch_cuda):
     for st in (sa, sb):
         order, cost = solid.schedule(rt.SCHED_SHADE, stream=st)
         _check_schedule(order, cost, "stream")
+
+
+def test_schedule_gated_on_camera_motion(worlds, torch_cuda):
+    """a frame whose camera turned more than 0.5 deg (or moved more than a voxel) since the last one runs the default
+    order and leaves no sorted order behind; the next frame near it sorts again"""
+    solid, _ = worlds
+    s = torch_cuda.cuda.Stream()
+    a, b = (1.0, -0.45, 1.0), (1.0, -0.45, 0.8)  # ~6 deg apart
+    ref_a = _shade(worlds, a, flags=rt.CAST_NO_SCHEDULE, stream=s)
+    ref_b = _shade(worlds, b, flags=rt.CAST_NO_SCHEDULE, stream=s)
+    for rep in range(3):
+        assert np.array_equal(_shade(worlds, a, stream=s), ref_a), "still %d" % rep
+    assert solid.schedule(rt.SCHED_SHADE, stream=s)[0] is not None
+    assert np.array_equal(_shade(worlds, b, stream=s), ref_b), "after the turn"
+    assert solid.schedule(rt.SCHED_SHADE, stream=s) == (None, None)  # (the turned frame was not sorted)
+    assert np.array_equal(_shade(worlds, b, stream=s), ref_b), "settled"
+    order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
+    _check_schedule(order, cost, "settled")
