@@ -15,6 +15,7 @@ svo_tree* g_tree = nullptr;   // solid view: castRayFromCam, primary frames, sha
 svo_tree* g_scene = nullptr;  // full view (water stored): what the shaded frame's rays walk (low_res.frag)
 bool g_rebuild = true;  // the world changed without a tree to patch (genWorld, edits before the first upload)
 svo_ray_result* g_look = nullptr;  // device record of the frame's lookingAtBlock pick ray (svoRenderShaded)
+int g_device = 0;  // the GPU the trees live on (initVoxelDataAllocator: SVO_DEVICE, default 0)
 
 void check(int rc, const char* what) {
     if (rc) {
@@ -100,15 +101,32 @@ void traverseTree(Pos* pos, int count) {
     for (int i = 0; i < count; i++) (void)getBlock(pos[i]);
 }
 
+// voxel_allocator.hpp:80-91, called once after initTetraHexaTree (main.cpp:183).  The reference creates its two
+// SSBOs here (bindings 2 and 3); the GPU side of the shim is the device the trees will live on: SVO_DEVICE
+// (default 0), checked to exist.  Nothing is uploaded yet: the world is empty until genWorld, and the first
+// updateSsboData (main.cpp:212) builds and uploads it
+void initVoxelDataAllocator() {
+    const char* e = getenv("SVO_DEVICE");
+    const int dev = e && *e ? atoi(e) : 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || dev >= n) {
+        fprintf(stderr, "svo_bridge: initVoxelDataAllocator: device %d not available (%d visible)\n", dev, n);
+        exit(1);
+    }
+    check(hipSetDevice(dev) == hipSuccess ? 0 : SVO_EDEVICE, "hipSetDevice");
+    if (g_tree && dev != g_device) g_rebuild = true;  // (a re-init onto another device re-uploads)
+    g_device = dev;
+}
+
 // voxel_allocator.hpp:38-78, called every frame (main.cpp:212): the first call (and any call after
 // genWorld) builds and uploads the tree; later calls upload only what edits changed
 void updateSsboData() {
     if (g_rebuild || !g_tree) {
         drop_trees();
         check(svo_build(g_world, &g_tree), "svo_build");
-        check(svo_upload(g_tree, 0), "svo_upload");
+        check(svo_upload(g_tree, g_device), "svo_upload");
         check(svo_build_view(g_world, SVO_VIEW_ALL, &g_scene), "svo_build_view");
-        check(svo_upload(g_scene, 0), "svo_upload");
+        check(svo_upload(g_scene, g_device), "svo_upload");
         g_rebuild = false;
         return;
     }

@@ -4,8 +4,10 @@
 //   initTetraHexaTree / putBlock / getBlock /
 //   deleteBlock / traverseTree                   src/voxel_data/tetrahexa_tree.hpp:12-22
 //   genWorld()                                   src/world_gen.hpp:3
-//   updateSsboData()                             src/voxel_data/voxel_allocator.hpp:38 (its inline GL
-//                                                body is replaced by this declaration)
+//   initVoxelDataAllocator() / updateSsboData()  src/voxel_data/voxel_allocator.hpp:38-91 (inline GL
+//                                                bodies in the original: the reference build swaps that
+//                                                header for bridge/reference/voxel_data/voxel_allocator.hpp,
+//                                                which only declares them)
 // The reference types (Pos, Block, RayResult, glm::vec3 cameraPos / cameraDir) come from
 // svo_bridge_types.hpp: bridge/reference/ (the reference's headers) in the reference build; the C++
 // test program (tests/bridge/) brings its own.
@@ -17,6 +19,7 @@
 #include "svo_bridge_types.hpp"
 #include "svo_rt.h"
 
+void initVoxelDataAllocator();
 void updateSsboData();
 
 // render() without GL (replaces glDrawArrays of the low_res program, src/main.cpp:105-107): one

@@ -58,24 +58,41 @@ def build(force=False, verbose=False, out=None, build_dir=None, defines=(), flag
     return OUT_
 
 
+def _bridge_cxx(root, rocm, incs):
+    return ["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(rocm, "include"),
+            "-I" + os.path.join(root, "include")] + ["-I" + i for i in incs]
+
+
 def build_bridge_test(force=False):
-    """The drop-in shim (bridge/svo_bridge.cpp) + its C++ test program (tests/bridge/bridge_test.cpp),
-    linked against libsvo_rt.so without Python: tests/bridge/_build/bridge_test."""
+    """The drop-in shim (bridge/svo_bridge.cpp) + its two C++ test programs, linked against libsvo_rt.so
+    without Python: tests/bridge/_build/bridge_test (the application's call sequence, edits, the exchange)
+    and tests/bridge/_build/main_shape (a main.cpp-shaped TU that includes the replacement
+    voxel_allocator.hpp, bridge/reference/voxel_data/; its object is kept for the nm check of
+    tests/test_bridge_link.py).  Returns the bridge_test path."""
     root = os.path.dirname(HERE)
     out_dir = os.path.join(root, "tests", "bridge", "_build")
-    out = os.path.join(out_dir, "bridge_test")
-    srcs = [os.path.join(root, "bridge", "svo_bridge.cpp"), os.path.join(root, "tests", "bridge", "bridge_test.cpp")]
-    deps = srcs + [os.path.join(root, "bridge", "svo_bridge.hpp"), os.path.join(root, "tests", "bridge", "svo_bridge_types.hpp"),
-                   os.path.join(root, "include", "svo_rt.h"), OUT]
-    if not force and not _newer(out, deps):
-        return out
     os.makedirs(out_dir, exist_ok=True)
     rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
-    _run(["g++", "-O2", "-std=c++17", "-Wall", "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(rocm, "include"),
-          "-I" + os.path.join(root, "include"), "-I" + os.path.join(root, "bridge"), "-I" + os.path.join(root, "tests", "bridge")] + srcs +
-         ["-L" + HERE, "-lsvo_rt", "-L" + os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath,$ORIGIN/../../../raytracing_test_amd",
-          "-Wl,-rpath," + os.path.join(rocm, "lib"), "-o", out])
-    return out
+    # tests/bridge first: its svo_bridge_types.hpp (the GLM-free mirror), not bridge/reference's
+    incs = [os.path.join(root, "tests", "bridge"), os.path.join(root, "bridge"), os.path.join(root, "bridge", "reference")]
+    hdrs = [os.path.join(root, "bridge", "svo_bridge.hpp"), os.path.join(root, "tests", "bridge", "svo_bridge_types.hpp"),
+            os.path.join(root, "bridge", "reference", "voxel_data", "voxel_allocator.hpp"), os.path.join(root, "include", "svo_rt.h")]
+    link = ["-L" + HERE, "-lsvo_rt", "-L" + os.path.join(rocm, "lib"), "-lamdhip64", "-Wl,-rpath,$ORIGIN/../../../raytracing_test_amd",
+            "-Wl,-rpath," + os.path.join(rocm, "lib")]
+    objs = {}
+    for name, src in (("svo_bridge", os.path.join(root, "bridge", "svo_bridge.cpp")),
+                      ("bridge_test", os.path.join(root, "tests", "bridge", "bridge_test.cpp")),
+                      ("main_shape", os.path.join(root, "tests", "bridge", "main_shape.cpp"))):
+        obj = os.path.join(out_dir, name + ".o")
+        if force or _newer(obj, [src] + hdrs):
+            _run(_bridge_cxx(root, rocm, incs) + ["-c", src, "-o", obj])
+        objs[name] = obj
+    for prog in ("bridge_test", "main_shape"):
+        out = os.path.join(out_dir, prog)
+        if force or _newer(out, [objs["svo_bridge"], objs[prog], OUT]):
+            # no voxel_allocator.cpp / tetrahexa_tree.cpp / ray_caster.cpp / world_gen.cpp: the shim and libsvo_rt only
+            _run(["g++", objs[prog], objs["svo_bridge"]] + link + ["-o", out])
+    return os.path.join(out_dir, "bridge_test")
 
 
 if __name__ == "__main__":

@@ -70,6 +70,44 @@ def test_bridge_sequence_vs_oracle(rt, oracle_mod, bridge_out):
     assert bridge_out["shade_dev_look_eq_host"] == 1  # the device look-at record (no host round trip) = the host pick
 
 
+MAIN = os.path.join(ROOT, "tests", "bridge", "_build", "main_shape")
+
+
+def test_main_shape_sequence_vs_oracle(rt, oracle_mod, tmp_path):
+    """main.cpp's own call sequence through the replacement voxel_allocator.hpp (tests/bridge/main_shape.cpp):
+    initTetraHexaTree -> initVoxelDataAllocator -> genWorld -> per frame updateSsboData + castRayFromCam(30)
+    + the shaded frame, with input.cpp's left / right clicks between frames; no voxel_allocator.cpp linked.
+    The picks and the last frame equal the oracle's after the same edits."""
+    assert os.path.exists(MAIN), "main_shape not built (raytracing_test_amd/build.py build_bridge_test)"
+    out = str(tmp_path / "main.json")
+    p = subprocess.run([MAIN, out], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, (p.stdout[-1000:], p.stderr[-2000:])
+    got = json.load(open(out))
+    assert got["tree_after_first_update"] == 1  # main.cpp:212 reached the shim's updateSsboData (build + upload)
+    T = oracle_mod.Tree.reference_world()
+    c, d = (35.0, 50.0, 35.0), oracle_mod.normalize((1.0, -1.0, 1.0))
+    red = 2097151 << 42  # hotbar[2]: RGB_TO_U64(255, 0, 0) (globals.cpp:47-51, types.hpp:8-9)
+
+    def left():  # input.cpp:141-151
+        r = T.cast_ray(c, d, 30)
+        if r.steps:
+            assert T.delete_block(*r.pos, level=6)[0] == 0
+
+    def right():  # input.cpp:154-159
+        r = T.cast_ray(c, d, 30)
+        assert T.put_block(*r.last, 0x2, red, 0.94, 6) == 0
+
+    for frame, click in enumerate((left, right, left, None)):
+        assert _got(got["pick_%d" % frame]) == _ray(T.cast_ray(c, d, 30)), frame
+        if click:
+            click()
+    assert got["pick_0"] != got["pick_1"]  # the first click deleted what the pick hit
+    ref = T.cast_frame(c, d, 64, 48, 300)
+    fr = np.array(got["frame"], np.int64).reshape(-1, 4)
+    assert np.array_equal(fr[:, :3], ref["pos"]) and np.array_equal(fr[:, 3], ref["steps"])
+    assert got["shade_finite"] == 1
+
+
 def test_bridge_single_rank_exchange(bridge_out):
     """svo_exchange_frames over a one-rank RCCL communicator: the unpacked frames equal the cast
     records bit for bit (hit records and AO counts)"""
