@@ -408,7 +408,10 @@ def main():
     ap.add_argument("--host-build", action="store_true", help="build the tree on the host (default: svo_build_terrain_gpu)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) or gloo (rehearsal on one GPU; torch exchange)")
     ap.add_argument("--verify", action="store_true",
-                    help="with an exchange: every rank checks the frames it displays against a one-GPU cast of them")
+                    help="with an exchange at N = 1 (--force-exchange): check the displayed frames against a one-GPU cast "
+                         "of them (at N > 1 this is the default)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N > 1: skip the check of the displayed frames after the timed region (gather_verified null)")
     ap.add_argument("--pipelined-steps", type=int, default=None,
                     help="N = 1: after the timed region, time this many more steps with consecutive launches on two "
                          "alternating streams (a launch's tail overlaps the next one's head), reported as `pipelined` "
@@ -512,9 +515,14 @@ def main():
     rays_per_launch = rt.Tree.count(desc)
     gather = (world > 1 or args.force_exchange) and not args.no_gather
     xmode = None
+    # the C-ABI exchange needs RCCL; a gloo rehearsal takes it too when SVO_RCCL_LIB names the test-only stand-in
+    # (tests/standin/rccl_standin.cpp: several ranks on one GPU, host-staged), else the torch exchange
+    standin = os.environ.get("SVO_RCCL_LIB") or None
     if gather:
-        xmode = "torch" if (args.shade or args.exchange == "torch" or args.dist_backend != "nccl") else "capi"
+        xmode = "torch" if (args.shade or args.exchange == "torch" or (args.dist_backend != "nccl" and not standin)) else "capi"
+    # tensors for the small control collectives: on the GPU over RCCL, on the host over gloo
     gdev = torch.device("cuda", dev)
+    cdev = gdev if args.dist_backend == "nccl" else torch.device("cpu")
     pipe_steps = args.steps if args.pipelined_steps is None else args.pipelined_steps
     if gather or world > 1 or args.inflight > 1:
         pipe_steps = 0  # (an N = 1 measurement beside the contract's own)
@@ -539,7 +547,7 @@ def main():
     if xmode == "capi":
         try:
             if world > 1:
-                uid = torch.zeros(rt.NCCL_UNIQUE_ID_BYTES, dtype=torch.uint8, device=gdev)
+                uid = torch.zeros(rt.NCCL_UNIQUE_ID_BYTES, dtype=torch.uint8, device=cdev)
                 if rank == 0:
                     uid.copy_(torch.frombuffer(bytearray(rt.Exchange.unique_id()), dtype=torch.uint8))
                 dist.broadcast(uid, 0)
@@ -554,7 +562,7 @@ def main():
         if world > 1:
             # every rank takes the same path: a rank whose exchange failed would otherwise wait in all_to_all while the
             # others wait in RCCL send / recv
-            ok = torch.tensor([1 if exch is not None else 0], dtype=torch.int32, device=gdev)
+            ok = torch.tensor([1 if exch is not None else 0], dtype=torch.int32, device=cdev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
             if int(ok.item()) == 0 and exch is not None:
                 torch.cuda.synchronize()
@@ -653,7 +661,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = [reg[0].elapsed_time(reg[1]) / args.steps] if region_events else [e[0].elapsed_time(e[1]) for e in evs]
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     total_rays = W * H * nframes * args.steps  # every rank's share of every frame, all steps
@@ -685,7 +693,8 @@ def main():
                             "itself runs longer, sharing the GPU: the per-launch roofline above is the one-at-a-time figure"}
 
     verified = None
-    if args.verify and gather and not args.shade:
+    # N > 1: one step's displayed frames against a one-GPU cast of them, after the timed region, by default
+    if (args.verify or (world > 1 and not args.no_verify)) and gather and not args.shade:
         torch.cuda.synchronize()
         ok = True
         for k, f in enumerate(range(rank, nframes, world)):
@@ -695,7 +704,7 @@ def main():
                 ok &= all(np.array_equal(got[key], one[key]) for key in got)
             else:
                 ok &= tx.verify(f, one)
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=gdev)
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
         if world > 1:
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         verified = bool(flag.item())
@@ -756,7 +765,8 @@ def main():
                        ("svo_cast_wire + svo_exchange_wire (C ABI, RCCL send/recv group): %d-B wire records written by the cast "
                         "kernel" % tree.wire_bytes(desc) + (" + AO counts" if args.ao else "") +
                         ", frame f to rank f % N (own shards decoded in place), decoded on arrival on a second stream "
-                        "overlapping the next cast")
+                        "overlapping the next cast" + (" — transport: the TEST-ONLY host-staged RCCL stand-in (SVO_RCCL_LIB=%s), "
+                                                        "not RCCL" % os.path.basename(standin) if standin else ""))
                        if xmode == "capi" else
                        ("torch.distributed all_to_all_single: " + ("rgba image" if args.shade else "12-B wire hit records") +
                         ", frame f to rank f % N" + ("; " + xnote if xnote else ""))),
@@ -764,7 +774,9 @@ def main():
                    "tree_builder": builder, **({"scene_nodes": scene.info().n_nodes} if scene is not None else {})},
         "roofline": roof,
         "cpu_baseline": cpu,
-        **({"gather_verified": verified} if verified is not None else {}),
+        **({"gather_verified": verified} if (verified is not None or world > 1) else {}),
+        **({"gather_verify_note": "the shaded image's exchange is not checked (gather_verified null)" if args.shade else
+            "--no-verify" if args.no_verify else "no exchange (--no-gather)"} if verified is None and world > 1 else {}),
         **({"pipelined": pipelined} if pipelined is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
                          "included" + ("; two frames in flight: the pair spans both cast streams" if inflight else "") + ")"

@@ -95,6 +95,24 @@ def build_bridge_test(force=False):
     return os.path.join(out_dir, "bridge_test")
 
 
+STANDIN = os.path.join(os.path.dirname(HERE), "tests", "standin", "_build", "librccl_standin.so")
+
+
+def build_rccl_standin(force=False):
+    """TEST-ONLY: tests/standin/rccl_standin.cpp -> tests/standin/_build/librccl_standin.so, the host-staged
+    stand-in for librccl.so.1 that libsvo_rt loads when SVO_RCCL_LIB names it (several ranks of the exchange on
+    one GPU).  Host code only; -Bsymbolic so its entry points never bind to an RCCL already in the process."""
+    src = os.path.join(os.path.dirname(HERE), "tests", "standin", "rccl_standin.cpp")
+    if not force and not _newer(STANDIN, [src]):
+        return STANDIN
+    os.makedirs(os.path.dirname(STANDIN), exist_ok=True)
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    _run([hipcc, "--offload-arch=" + ARCH, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+          "-Wl,-Bsymbolic", src, "-o", STANDIN])
+    return STANDIN
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
     build_bridge_test(force="--force" in sys.argv)
+    build_rccl_standin(force="--force" in sys.argv)

@@ -19,6 +19,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -56,17 +57,22 @@ Rccl& rccl() {
     static Rccl R;
     static std::once_flag once;
     std::call_once(once, [] {
-        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        // SVO_RCCL_LIB: another library with RCCL's entry points instead (tests/standin/rccl_standin.cpp, the test-only
+        // stand-in that runs the N > 1 pairing with several ranks on one GPU), loaded locally so it shadows nothing
+        const char* over = getenv("SVO_RCCL_LIB");
+        const bool o = over && *over;
+        const std::string name = o ? over : "librccl.so.1";
+        void* h = dlopen(name.c_str(), o ? (RTLD_NOW | RTLD_LOCAL) : (RTLD_NOW | RTLD_GLOBAL));
         if (!h) {
-            R.err = std::string("cannot load librccl.so.1: ") + dlerror();
+            R.err = "cannot load " + name + ": " + dlerror();
             return;
         }
         bool all = true;
-        auto sym = [&](auto& fn, const char* name) {
-            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        auto sym = [&](auto& fn, const char* sname) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, sname));
             if (!fn) {
                 all = false;
-                R.err = std::string("librccl.so.1 lacks ") + name;
+                R.err = name + " lacks " + sname;
             }
         };
         sym(R.GetUniqueId, "ncclGetUniqueId");

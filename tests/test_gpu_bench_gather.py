@@ -69,3 +69,41 @@ def test_launcher_free_two_ranks_verified():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
     assert d["gather_verified"] is True, d
+
+
+STANDIN = os.path.join(ROOT, "tests", "standin", "_build", "librccl_standin.so")
+
+
+@pytest.mark.parametrize("n,extra", [
+    (2, ()),                               # weak C3: frame f -> rank f, one all-to-all group per step
+    (3, ()),
+    (2, ("--frames", "1")),                # strong: one frame over N ranks, gathered to rank 0
+    (3, ("--frames", "1")),
+    (2, ("--ao", "16")),                   # C4's AO counts travel beside the records
+    (3, ("--frames", "1", "--ao", "16")),
+])
+def test_capi_exchange_on_one_gpu(n, extra, tmp_path):
+    """The C-ABI exchange's N > 1 code — svo_cast_wire + svo_exchange_wire, its ncclGroupStart / ncclSend / ncclRecv /
+    ncclGroupEnd pairing and the display-side decode of every received shard — with N ranks on one GPU: libsvo_rt
+    loads the test-only host-staged stand-in (SVO_RCCL_LIB, tests/standin/rccl_standin.cpp) in place of RCCL,
+    which cannot form a communicator of two ranks on one device.  bench.py verifies every displayed frame against a
+    one-GPU cast by default at N > 1."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert os.path.exists(STANDIN), "the stand-in is not built (raytracing_test_amd/build.py build_rccl_standin)"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(SVO_RCCL_LIB=STANDIN, SVO_STANDIN_DIR=str(tmp_path), SVO_STANDIN_TIMEOUT_S="60")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dist-backend", "gloo", "--exchange", "capi",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"] + list(extra)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n  # svo_exchange_info of the communicator the step ran over
+    assert d["config"]["exchange"].startswith("svo_cast_wire + svo_exchange_wire") and "stand-in" in d["config"]["exchange"], d
+    assert d["scaling"] == ("strong" if "--frames" in extra else "weak")
+    assert d["gather_verified"] is True, d
+    assert [x for x in os.listdir(tmp_path) if x.startswith("svo_rccl_standin_")] == []  # every message was received
