@@ -237,7 +237,7 @@ def cpu_c1(O, nt):
 
 
 # ---------------------------------------------------------------------------------- roofline --
-def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
+def roofline(args, cfg, rays_per_launch, avg_kernel_s, world, lib_sha):
     """The kernel against the HBM roofline (the contract's "bound": "hbm" — pointer chasing, no MFMA).
     achieved = algorithmic bytes per ray x rays per launch / average launch time.  Primary rays: SURVEY.md
     §8(d)'s B_ray (node entries along the reference DDA path, oracle/bray.py).  C4: that, plus the node
@@ -292,6 +292,13 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
             "bytes_per_ray": round(model, 2) if model else None, "bytes_model": bytes_model,
             "avg_launch_ms": round(avg_kernel_s * 1e3, 4), "rays_per_launch": rays_per_launch, **extra}
     pmc = load_json("pmc_%s.json" % run_key(args))
+    if pmc and pmc.get("rays_per_launch") and pmc.get("lib_sha256") != lib_sha:
+        # counters of another build: they say nothing about the kernel timed here
+        roof["counters"] = ("stale: profiles/pmc_%s.json was measured on libsvo_rt.so %s, this run loads %s; traffic, L2 hit "
+                            "rate and instruction counts omitted" % (run_key(args), (pmc.get("lib_sha256") or "(unrecorded)")[:12],
+                                                                     lib_sha[:12]))
+        roof["counters_build"] = pmc.get("lib_sha256")
+        pmc = None
     if pmc and pmc.get("rays_per_launch"):
         c = pmc["counters_per_dispatch"]
         scale = rays_per_launch / pmc["rays_per_launch"]  # per-ray figures of the N=1 pass, this launch's rays
@@ -305,8 +312,9 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world):
             "valu_insts_per_wave": round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"], 1),
             "salu_insts_per_wave": round(c["SQ_INSTS_SALU"] / c["SQ_WAVES"], 1) if "SQ_INSTS_SALU" in c else None,
             "valu_issue_frac": round(valu_frac, 4),
-            "counters": "profiles/pmc_%s.json (rocprofv3 --pmc passes, tools/pmc.sh%s)" % (run_key(args), "; scaled per ray to this launch"
-                                                                                          if world > 1 or scale != 1 else ""),
+            "counters": "profiles/pmc_%s.json (rocprofv3 --pmc passes, tools/pmc.sh%s), measured on this build" % (
+                run_key(args), "; scaled per ray to this launch" if world > 1 or scale != 1 else ""),
+            "counters_build": pmc["lib_sha256"],
             "valu_issue_rule": "SQ_INSTS_VALU x %d cycles / (%d SIMDs x %.1f GHz x launch time)" % (VALU_CYCLES, N_SIMD, CLOCK_GHZ),
         })
         if all(k in c for k in ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")):
@@ -722,7 +730,8 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    roof = roofline(args, cfg, rays_per_launch, avg_kernel_s, world)
+    roof = roofline(args, cfg, rays_per_launch, avg_kernel_s, world, rt.lib_sha256())
+    roof["timed_build"] = rt.lib_sha256()
     cpu = None
     if world == 1 and nframes == 1 and not args.no_cpu_baseline:
         gpu = None
@@ -774,6 +783,7 @@ def main():
                    "tree_builder": builder, **({"scene_nodes": scene.info().n_nodes} if scene is not None else {})},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "build": {"libsvo_rt_sha256": rt.lib_sha256(), "library": os.path.relpath(rt.LIB_PATH, ROOT)},
         **({"gather_verified": verified} if (verified is not None or world > 1) else {}),
         **({"gather_verify_note": "the shaded image's exchange is not checked (gather_verified null)" if args.shade else
             "--no-verify" if args.no_verify else "no exchange (--no-gather)"} if verified is None and world > 1 else {}),

@@ -154,7 +154,8 @@ int svo_upload(svo_tree* t, int32_t device);
    of it.  Host only; svo_tree_sync brings the device copy up to date. */
 int svo_tree_update(svo_tree* t, const svo_world* w, const int32_t* xyz, int64_t n, int32_t level);
 /* upload what svo_tree_update changed: the appended tail and the rewritten records (or everything
-   after a rebuild / when the device allocation is outgrown) */
+   after a rebuild / when the device allocation is outgrown).  Synchronises the device first (device
+   memory is rewritten in place): call it between frames, as updateSsboData is (main.cpp:212). */
 int svo_tree_sync(svo_tree* t);
 void svo_tree_destroy(svo_tree* t);
 /* The column ceilings the casts use (SVO_CAST_NO_CEILINGS): for k = SVO_CEIL_K0 .. min(levels - 1, SVO_CEIL_K0 + 3)
@@ -300,7 +301,8 @@ int svo_cast_ray_from_cam(const svo_tree* t, const float pos[3], const float dir
                           svo_block* block);
 /* Launches over t whose rays ended on the traversal's progress guard (an iteration that took no DDA step:
    only a wrong crossing count can cause it).  Such a ray's record has stepsLeft = -1 and no hit; the count
-   should be 0.  reset != 0 zeroes the counter.  Synchronous (reads device memory). */
+   should be 0 (shading launches count on t, the tree their shadow rays walk).  reset != 0 zeroes the counter.
+   Synchronous: waits for the whole device (launches on any stream), then reads device memory. */
 int svo_tree_guard_trips(const svo_tree* t, uint64_t* trips, int32_t reset);
 /* the same pick ray, stream-ordered and without a host round trip: the result (svo_ray_result, 28 B) is
    written to d_result, device memory aligned to 16 bytes, on hip_stream (two small launches) — for the

@@ -149,6 +149,22 @@ ABI_SYMBOLS = (
 )
 
 
+_lib_sha = None
+
+
+def lib_sha256():
+    """sha256 of the libsvo_rt.so this process loads (LIB_PATH): the build a measurement belongs to (bench.py puts it on
+    its line; tools/pmc_summary.py records it with the PMC counters, and bench.py uses committed counters only when
+    they were measured on the same build)."""
+    global _lib_sha
+    if _lib_sha is None:
+        import hashlib
+
+        with open(LIB_PATH, "rb") as f:
+            _lib_sha = hashlib.sha256(f.read()).hexdigest()
+    return _lib_sha
+
+
 def lib():
     """Load libsvo_rt.so (raises if it has not been built: there is no fallback path)."""
     global _lib

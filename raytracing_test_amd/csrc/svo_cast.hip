@@ -81,6 +81,7 @@ struct CastParams {
     float sun[3];
     int32_t look[3];
     int32_t look_valid, shadow_steps;
+    int32_t look_empty;         // the host look-at voxel is not stored in the scene (an escaped ray could end on it)
     const int32_t* look_dev;    // device lookingAtBlock record (svo_ray_result: pos first) or null
     float time;                 // deltaTime of the liquid wobble (low_res.frag:226)
     const Node* snodes;         // shading: the solid-view tree the shadow rays walk (nodes: the scene)
@@ -96,6 +97,8 @@ struct CastParams {
     uint32_t ceil_sh[2];
     int64_t ceil_off[2];
     const uint32_t* ceilp;  // the launch's two levels paired (svo_tree.d_ceilp at its first level's offset)
+    const uint32_t* sceilp;  // shading: the same pairs of the solid-view tree the shadow rays walk (trace CEIL 3)
+    int32_t sceil_levels;
     const uint64_t* ceilq;  // every level per finest block (svo_tree.d_ceilq; trace CEIL == 2)
     uint32_t* guard_trips;  // the tree's counter of progress-guard trips (svo_tree_guard_trips)
     // frame schedule (sched_attach): launch block b casts frame block sched_order[b] (null: b) and, with sched_cost,
@@ -501,6 +504,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // brick holding the voxel (mask / ref / info returned).  tetrahexa_tree.cpp:124-152 on the
 // breadth-first layout.
 enum : uint32_t { R_EMPTY = 0u, R_BRICK = 1u, R_SOLID = 2u, R_CEIL = 3u };
+// Hit.info of a shading ray that left the loop early (ESCAPE): a miss whose remaining steps are all in empty voxels
+// (never written to a hit record: escaping is off when records are requested)
+constexpr uint32_t ESC_BIT = 1u << 19;
 
 // The interior node whose child region holds the ray's current cell, kept in registers: a move to
 // a sibling region reads the cached child mask (no load when the sibling is empty) and restarts
@@ -881,8 +887,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
     // CEIL 1: the launch's two levels of the column ceilings (P.ceilp pairs); 2: every level, the coarsest block the ray is
-    // above (P.ceilq: a max-mipmap walk of the ceilings)
-    const bool ceil_on = CEIL != 0 && P.ceil_levels > 0;  // (uniform)
+    // above (P.ceilq: a max-mipmap walk of the ceilings); 3: as 1 on P.sceilp
+    // (CEIL 3: CEIL 1 on the pairs of the solid-view tree of a shading launch, P.sceilp — the shadow rays)
+    const bool ceil_on = CEIL != 0 && (CEIL == 3 ? P.sceil_levels : P.ceil_levels) > 0;  // (uniform)
+    const uint32_t* const ceilp = CEIL == 3 ? P.sceilp : P.ceilp;
     uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 16-column block (key) and its ceilings (c0 | c1 << 16)
     uint64_t cq = 0ull;                      // (CEIL 2: the ceilings of the blocks of every level holding the lane's 16-column block)
     while (!done) {
@@ -935,7 +943,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // ceilings come from one 32-bit load of svo_tree.d_ceilp: the block's ceiling and its parent block's)
             if (key != ckey) {
                 ckey = key;
-                cval = P.ceilp[key];
+                cval = ceilp[key];
             }
             c0 = (int32_t)(int16_t)(cval & 0xFFFFu);
             c1 = (int32_t)cval >> 16;
@@ -1254,6 +1262,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     const int32_t sa = R.axis == 0u ? R.s[0] : (R.axis == 1u ? R.s[1] : R.s[2]);
     const uint32_t neg = (R.axis < 3u && sa < 0) ? 1u : 0u;
     h.info = (hit ? HIT_BIT : 0u) | (R.axis << AXIS_SHIFT) | (neg ? NEG_BIT : 0u) | (hit ? mat & MAT_MASK : 0u);
+    if (ESCAPE && escaped) h.info |= ESC_BIT;  // (its position is where the escape began, not where the budget ends)
     return h;
 }
 
@@ -1392,7 +1401,9 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
         lk[2] = P.look_dev[2];
         lv = true;
     }
-    if (lv && h.x == lk[0] && h.y == lk[1] && h.z == lk[2]) {
+    // (an escaped ray's position is not its end; it can only end on a voxel the scene does not store, and the launch lets
+    // rays escape only when the look-at voxel is stored: k_cast's `esc`)
+    if (lv && !(h.info & ESC_BIT) && h.x == lk[0] && h.y == lk[1] && h.z == lk[2]) {
         const float3 b = color_of(P.mat_color[hit ? (h.info & MAT_MASK) : 0u]);
         c = make_float3(b.x * 2.0f + 0.3f, b.y * 2.0f + 0.3f, b.z * 2.0f + 0.3f);
     } else if (!hit) {
@@ -1415,7 +1426,7 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
                 const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                      (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
                 // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
-                dark = (trace<false, false, true, false, DIRS, false, 1>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
+                dark = (trace<false, false, true, false, DIRS, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                             .info & HIT_BIT) != 0u;
             }
         }
@@ -1514,9 +1525,15 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
         // it cost the loop spills (22 VGPRs at 8 waves; 0.4748 -> 0.4660 ms per shaded C3 frame at 5 waves without them)
         Bounce& bn = shade_bn[threadIdx.x];
         bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
+        // rays may escape (stop early once only empty voxels lie ahead) unless their end position is output (hit records)
+        // or could be the highlighted lookingAtBlock (low_res.frag:347 compares every ray's end, misses too): a look-at
+        // voxel the scene may not store — the host's, checked on the host, or a device pick record that is not a sure hit
+        // (stepsLeft 0: a miss or a hit on the last step) (uniform)
+        const bool look_risk = P.look_dev ? P.look_dev[6] <= 0 : (P.look_valid && P.look_empty);
+        const int32_t esc = (P.pos || look_risk) ? -1 : P.top_scene;
         const Hit h = trace<STATS, true, true, SEG, 0, false, 2>(
             P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
-            &bn, nullptr, P.pos ? -1 : P.top_scene, P.top_scene);
+            &bn, nullptr, esc, P.top_scene);
         shade_out<DIRS>(P, smem, path, h, bn, out);
     } else if (out >= 0) {
         Parent pfin;
@@ -1945,12 +1962,16 @@ struct SchedUse {  // a launch's schedule (sched_attach), by value: the tree's l
     int64_t blocks = 0;
     int32_t kind = 0;
 };
-SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, int32_t kind, int64_t blocks, hipStream_t st) {
+// `lock` (the tree's sched_mu) is taken here and stays held by the caller until the launch and its sort are queued
+// (sched_order): the buffer handed out cannot be freed by another thread's eviction or resize before the work that uses
+// it is on its stream (hipFree synchronises the device, which protects queued work only)
+SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, int32_t kind, int64_t blocks, hipStream_t st,
+                      std::unique_lock<std::mutex>& lock) {
     if (P.mode != MODE_FRAME || (P.flags & (SVO_CAST_NO_SCHEDULE | SVO_CAST_STATS)) || blocks <= SVO_SCHED_MIN_BLOCKS ||
         blocks > 0x7FFFFFFFll || blocks % kSchedGroup)
         return SchedUse{};
     const int64_t sig[7] = {P.width, P.height, P.n_frames, P.tile_row_start, P.tile_row_step, P.tile_lh, (int64_t)(P.flags & SVO_CAST_BOTTOM_FIRST)};
-    std::lock_guard<std::mutex> lock(t->sched_mu);
+    lock = std::unique_lock<std::mutex>(t->sched_mu);
     svo_tree::Sched* s = nullptr;
     for (auto& e : t->scheds)
         if (e.stream == (void*)st && e.kind == kind) s = &e;
@@ -1994,12 +2015,12 @@ SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, 
     }
     return SchedUse{base, blocks, kind};
 }
-// after the launch of a scheduled frame: the next frame's order (the schedule counts as sorted once the sort is queued)
+// after the launch of a scheduled frame: the next frame's order (the schedule counts as sorted once the sort is queued);
+// called with sched_attach's lock still held
 int sched_order(const svo_tree* t, const SchedUse& u, hipStream_t st) {
     if (!u.base) return SVO_OK;
     hipLaunchKernelGGL(k_sched_order, dim3(1), dim3(kSchedThreads), 0, st, u.base + u.blocks, u.base, (uint32_t)(u.blocks / kSchedGroup));
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
-    std::lock_guard<std::mutex> lock(t->sched_mu);
     for (auto& e : t->scheds)
         if (e.stream == (void*)st && e.kind == u.kind && e.d_buf == (void*)u.base && e.blocks == u.blocks) e.primed = true;
     return SVO_OK;
@@ -2258,6 +2279,10 @@ extern "C" int svo_tree_sync(svo_tree* t) {
         t->ceil_dirty.empty())
         return SVO_OK;  // nothing changed since the last upload / sync
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
+    // the records, ceilings and palette below are rewritten in place: every cast over the tree must be over first, on any
+    // stream (null-stream copies do not wait for non-blocking streams; a frame reading lowered ceilings against old nodes
+    // could skip blocks still stored).  As the reference's updateSsboData, this runs between frames.
+    HIP_TRY(hipDeviceSynchronize(), SVO_EDEVICE);
     Node* dn = reinterpret_cast<Node*>(t->d_nodes);
     if (t->nodes.size() > t->synced_nodes)
         HIP_TRY(hipMemcpy(dn + t->synced_nodes, t->nodes.data() + t->synced_nodes, (t->nodes.size() - t->synced_nodes) * sizeof(Node),
@@ -2311,6 +2336,16 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     int rc = fill_params(sc, d, o ? o : &none, P, n);
     if (rc) return rc;
     set_ceilings(sc, d, P, kCeilShade);
+    // shadow rays walk t: its own column ceilings (the scene's hold for the scene's voxels, which is t's world only when
+    // both trees are synced to the same edits), and t's guard-trip counter (svo_tree_guard_trips counts launches over t)
+    {
+        CastParams S;
+        set_ceilings(t, d, S, kCeilShade);
+        const bool same = S.ceil_levels == P.ceil_levels && S.ceil_sh[0] == P.ceil_sh[0] && S.ceil_sh[1] == P.ceil_sh[1];
+        P.sceilp = same ? S.ceilp : nullptr;
+        P.sceil_levels = same ? S.ceil_levels : 0;  // (shadow rays then walk the tree)
+    }
+    P.guard_trips = guard_word(t);
     P.snodes = reinterpret_cast<const Node*>(t->d_nodes);
     P.smats = reinterpret_cast<const uint16_t*>(t->d_mats);
     P.time = sd->time;
@@ -2322,6 +2357,13 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         P.look[k] = sd->look_at[k];
     }
     P.look_valid = sd->look_at_valid != 0;
+    if (P.look_valid && !sd->look_at_dev) {
+        svo_block b;
+        uint32_t mid = 0;
+        rc = svo_tree_get_block(sc, sd->look_at[0], sd->look_at[1], sd->look_at[2], &b, &mid);
+        if (rc) return rc;
+        P.look_empty = mid == 0u;  // (palette entry 0: no block)
+    }
     P.look_dev = reinterpret_cast<const int32_t*>(sd->look_at_dev);
     P.shadow_steps = sd->shadow_steps;
     if (n == 0) return SVO_OK;
@@ -2335,7 +2377,8 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         else if (!(P.sun[k] > 0.0f)) sun_dirs = 0;
     }
     const bool wide = wide_nodes(t, d->flags) || wide_nodes(sc, d->flags);
-    const SchedUse sch = sched_attach(t, d, P, 2, blocks, (hipStream_t)stream);
+    std::unique_lock<std::mutex> sched_lock;  // (held from here until the launch and the sort are queued)
+    const SchedUse sch = sched_attach(t, d, P, 2, blocks, (hipStream_t)stream, sched_lock);
     if (P.flags & SVO_CAST_STATS) launch_cast<true, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     else if (P.flags & SVO_CAST_TIMELINE) launch_cast<false, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     else launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, sun_dirs);
@@ -2536,6 +2579,8 @@ extern "C" int svo_tree_guard_trips(const svo_tree* t, uint64_t* trips, int32_t 
     if (t->device < 0) SVO_FAIL(SVO_ESTATE, "svo_tree_guard_trips: tree not uploaded (svo_upload)");
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     uint32_t v = 0;
+    // every launch over t finished, on whatever stream (a null-stream copy does not wait for non-blocking streams)
+    HIP_TRY(hipDeviceSynchronize(), SVO_EDEVICE);
     HIP_TRY(hipMemcpy(&v, guard_word(t), sizeof(v), hipMemcpyDeviceToHost), SVO_EDEVICE);
     if (reset) HIP_TRY(hipMemset(guard_word(t), 0, sizeof(v)), SVO_EDEVICE);
     *trips = v;

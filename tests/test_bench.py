@@ -48,30 +48,44 @@ def test_run_keys(bench):
 def test_roofline_model_and_counters(bench):
     cfg = bench.CONFIGS["c3"]
     bray = json.load(open(os.path.join(ROOT, "profiles", "bray.json")))
-    r = bench.roofline(_args(), cfg, 2073600, 0.23e-3, 1)
+    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_c3.json")))
+    sha = pmc["lib_sha256"]  # the counters' build: used as if this run loaded it
+    r = bench.roofline(_args(), cfg, 2073600, 0.23e-3, 1, sha)
     b = bray["C3"]["bytes_per_ray"]
     assert abs(r["bytes_per_ray"] - b) < 0.01
     assert abs(r["achieved"] - b * 2073600 / 0.23e-3 / 1e9) < 0.01
     assert abs(r["frac"] - r["achieved"] / 8000.0) < 1e-4
-    pmc = json.load(open(os.path.join(ROOT, "profiles", "pmc_c3.json")))
     assert r["traffic"] == round(pmc["hbm_bytes_per_launch"])  # the same rays per launch: unscaled
+    assert r["counters_build"] == sha and "measured on this build" in r["counters"]
     assert r["bound"] == "hbm" and "wait to issue" in r["limiter"]  # (the contract's roofline; the SQ counters name the limiter)
     # C4: the primary bytes + the AO plan's node loads (not the traced-AO model, which is reported beside it)
-    r4 = bench.roofline(_args(ao=16), cfg, 2073600, 0.31e-3, 1)
+    r4 = bench.roofline(_args(ao=16), cfg, 2073600, 0.31e-3, 1, sha)
     kb = bray["C4_ao16_kernel"]["ao_node_loads_per_ray"]
     assert abs(r4["bytes_per_ray"] - (b + 16 * kb + 1)) < 0.01 and r4["bytes_per_ray"] > r["bytes_per_ray"]
     assert abs(r4["bytes_per_ray_traced_ao_model"] - bray["C4_ao16"]["bytes_per_ray"]) < 0.01
     # a fraction above 1 is never published
-    rf = bench.roofline(_args(), cfg, 2073600, 0.05e-3, 1)
+    rf = bench.roofline(_args(), cfg, 2073600, 0.05e-3, 1, sha)
     assert rf["frac"] is None and "withheld" in rf["note"]
-    rs = bench.roofline(_args(shade=True), cfg, 2073600, 1.3e-3, 1)
+    rs = bench.roofline(_args(shade=True), cfg, 2073600, 1.3e-3, 1, sha)
     # the shading pass: priced by its own §8(d) entries (oracle/bray.py C3_shade)
     sb = bray["C3_shade"]
     assert abs(rs["bytes_per_ray"] - sb["bytes_per_ray"]) < 0.01 and "shading pass" in rs["bytes_model"]
     assert abs(rs["frac"] - sb["bytes_per_ray"] * 2073600 / 1.3e-3 / 1e9 / 8000.0) < 1e-4
     # counters measured at N = 1 scale per ray to another launch size (a rank's shard)
-    rh = bench.roofline(_args(), cfg, 2073600 // 2, 0.12e-3, 2)
+    rh = bench.roofline(_args(), cfg, 2073600 // 2, 0.12e-3, 2, sha)
     assert rh["traffic"] == round(pmc["hbm_bytes_per_launch"] / 2)
+    # counters of another build are not used: marked stale, no traffic
+    rx = bench.roofline(_args(), cfg, 2073600, 0.23e-3, 1, "0" * 64)
+    assert rx["traffic"] is None and rx["counters"].startswith("stale") and "limiter" not in rx
+
+
+def test_committed_counters_name_their_build():
+    """every committed PMC summary records the libsvo_rt.so it was measured on (tools/pmc_summary.py)"""
+    import glob
+
+    for f in glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")):
+        d = json.load(open(f))
+        assert len(d.get("lib_sha256") or "") == 64, f
 
 
 @pytest.mark.parametrize("world,nframes", [(1, 1), (2, 1), (2, 2), (3, 2), (3, 5), (4, 4), (8, 8), (8, 1)])

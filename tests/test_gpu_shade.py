@@ -297,3 +297,90 @@ def test_shade_bench_scene_full_frame(rt, depth12, oracle12, torch_cuda):
     wet = int((dry != img).any(1).sum().item())
     assert wet > 100000, wet  # lake pixels: tinted and refracted
     del scene
+
+
+def test_shadow_rays_use_the_solid_trees_ceilings(rt, torch_cuda):
+    """Shadow rays walk the solid tree, so they cross the solid tree's own column-ceiling boxes (trace CEIL 3), not the
+    scene's: with the scene one edit behind (a 4^3 block put above the 16-column block's old ceiling, the solid tree
+    synced, the scene not), the image equals the one rendered without ceilings (SVO_CAST_NO_CEILINGS: ceilings are an
+    exact acceleration), and the new block's shadow shows.  (Round 4 used the scene's table: shadow rays jumped over
+    the new block.)"""
+    torch = torch_cuda
+    w = rt.World.reference()
+    t = w.build().upload(0)
+    sc = w.build(rt.VIEW_ALL).upload(0)
+    org, cam_dir = (50.0, 70.0, 40.0), rt.normalize((20.0, -28.0, 25.0))
+    W, H, S = 160, 120, 300
+    before = t.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), scene=sc)
+    w.put_block(72, 46, 72, 0, 777, level=5)  # rows 44-47 over columns (72..75, 72..75); the block's ceiling was 43
+    t.update(w, np.array([[72, 46, 72]], np.int32), level=5)
+    t.sync()  # the scene lags
+    a = t.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), scene=sc)
+    b = t.shade_frame(org, cam_dir, W, H, S, sun=rt.sun_dir(), scene=sc, flags=rt.CAST_NO_CEILINGS)
+    assert torch.equal(a, b)
+    assert int((a != before).any(1).sum()) > 50  # the shadow (the lagging scene does not draw the block itself)
+
+
+def test_shade_escape_and_look_at(rt, gtree, lake_scene, torch_cuda):
+    """An escaped ray (no hit records: it stops once only empty voxels lie ahead) keeps the position where it escaped,
+    but low_res.frag:347 compares every ray's END with lookingAtBlock, misses included.  A launch whose look-at voxel
+    the scene may not store — a host look-at on an empty voxel, or a device pick record that is not a sure hit —
+    lets no ray escape; with a hit pick, escaped rays skip the comparison (they end on empty voxels only).  Each image
+    equals the one rendered with hit records (where no ray escapes), and the highlight of a miss's end voxel shows."""
+    torch = torch_cuda
+    s = torch.cuda.Stream()
+    org, cam_dir = (4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0))
+    W, H, S = 200, 120, 300
+    sun = rt.sun_dir()
+    full, hits = gtree.shade_frame(org, cam_dir, W, H, S, sun=sun, with_hits=True, scene=lake_scene)
+    g = rt.decode_hits(hits)
+    miss = np.nonzero(~g["hit"])[0]
+    assert len(miss) > 100
+    # host look-at on the end voxel of a miss (an empty voxel): the reference highlights that pixel
+    p = int(miss[len(miss) // 2])
+    look = tuple(int(v) for v in g["pos"][p])
+    ref, _ = gtree.shade_frame(org, cam_dir, W, H, S, sun=sun, look_at=look, with_hits=True, scene=lake_scene)
+    fast = gtree.shade_frame(org, cam_dir, W, H, S, sun=sun, look_at=look, scene=lake_scene)
+    assert torch.equal(ref, fast)
+    assert bool((ref[p] != full[p]).any())
+    # the device record of a pick along a missing pixel's own ray with the frame's budget: a miss (stepsLeft 0) that
+    # ends on that pixel's end voxel
+    ppx, ppy = rt.proj_plane(W, H)
+    rec = torch.zeros(64, dtype=torch.int32, device="cuda")
+    desc = gtree.frame_desc(org, cam_dir, W, H, S)
+    found = 0
+    for p in miss[::max(1, len(miss) // 40)]:
+        p = int(p)
+        d = rt.pixel_dir(cam_dir, ppx, ppy, W, H, p % W, p // W)
+        gtree.cast_ray_from_cam_async(org, d, S, rec, stream=s)
+        s.synchronize()
+        r = rec[:7].cpu().numpy()
+        if tuple(r[:3]) != tuple(g["pos"][p]) or r[6] != 0:
+            continue  # (a ray bent by water in the scene ends elsewhere)
+        a = torch.empty((W * H, 4), dtype=torch.float32, device="cuda")
+        b = torch.empty_like(a)
+        out = gtree.alloc_hits(W * H, 0)
+        with torch.cuda.stream(s):
+            gtree.shade(desc, a, sun=sun, look_at=rec, stream=s, scene=lake_scene)
+            gtree.shade(desc, b, sun=sun, look_at=rec, out=out, stream=s, scene=lake_scene)
+        s.synchronize()
+        assert torch.equal(a, b), p
+        assert bool((a[p] != full[p]).any()), p
+        found += 1
+        if found == 3:
+            break
+    assert found > 0
+    # a sure hit (stepsLeft 15 > 0): rays escape and escaped ones skip the comparison
+    org2, cam2 = (35.0, 50.0, 35.0), rt.normalize((1.0, -1.0, 1.0))
+    gtree.cast_ray_from_cam_async(org2, cam2, 30, rec, stream=s)
+    s.synchronize()
+    assert int(rec[6]) == 15
+    d2 = gtree.frame_desc(org2, cam2, W, H, S)
+    a = torch.empty((W * H, 4), dtype=torch.float32, device="cuda")
+    b = torch.empty_like(a)
+    out = gtree.alloc_hits(W * H, 0)
+    with torch.cuda.stream(s):
+        gtree.shade(d2, a, sun=sun, look_at=rec, stream=s, scene=lake_scene)
+        gtree.shade(d2, b, sun=sun, look_at=rec, out=out, stream=s, scene=lake_scene)
+    s.synchronize()
+    assert torch.equal(a, b)

@@ -62,6 +62,8 @@ def main(out, bench_args=""):
     if h is not None and m is not None and h + m > 0:
         res["l2_hit_rate"] = h / (h + m)
     b = bench_line(out)
+    # the build the passes ran (bench.py's line): bench.py reads these counters only for the same libsvo_rt.so
+    res["lib_sha256"] = (b or {}).get("build", {}).get("libsvo_rt_sha256")
     if b and b.get("roofline"):
         res["rays_per_launch"] = b["roofline"]["rays_per_launch"]
         res["bench_avg_launch_ms"] = b["roofline"]["avg_launch_ms"]
