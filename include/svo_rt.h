@@ -164,9 +164,15 @@ void svo_tree_destroy(svo_tree* t);
    4^(SVO_CEIL_K0 + j) columns wide).  out may be NULL (count only); levels = number of levels, n = elements. */
 #define SVO_CEIL_K0 2
 int svo_tree_ceilings(const svo_tree* t, int16_t* out, int64_t cap, int32_t* levels, int64_t* n);
+/* The pairs the casts read: level j's block ceiling with that of the level min(j + SVO_CEIL_PAIR_STEP, levels - 1)
+   block holding it (primary casts and shadow rays check levels 0 and SVO_CEIL_PAIR_STEP of the table) */
+#define SVO_CEIL_PAIR_STEP 1
+/* the ceiling layout this library was built with: SVO_CEIL_K0 and SVO_CEIL_PAIR_STEP (either may be NULL) */
+int svo_ceiling_layout(int32_t* k0, int32_t* pair_step);
 /* The column-ceiling tables in HBM as the casts read them (inspection / tests): the int16 ceilings in
-   svo_tree_ceilings' layout and their uint32 pairs (low: the block's ceiling, high: its next-level block's; the
-   last level paired with itself).  levels = 0 when the tree has none.  Either buffer may be NULL. */
+   svo_tree_ceilings' layout and their uint32 pairs (low: the block's ceiling, high: the ceiling of the level
+   j + SVO_CEIL_PAIR_STEP block holding it, the coarsest level there is).  levels = 0 when the tree has none.
+   Either buffer may be NULL. */
 int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32_t* pairs, int64_t cap, int32_t* levels, int64_t* n);
 /* The per-level quads in HBM (the shading pass's walk over every ceiling level): for every block of the finest
    level (4^SVO_CEIL_K0 columns, row-major [z][x]), the ceilings of the blocks of levels 0..3 holding it, int16 each,

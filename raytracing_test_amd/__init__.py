@@ -54,7 +54,7 @@ STAT_NAMES = ("rays", "lookups", "node_loads", "skips", "skip_budget_out", "bric
 STATS_HEADER = 32  # u64 counters before the per-block stamps (SVO_STATS_HEADER)
 MAX_FRAMES = 16  # SVO_MAX_FRAMES: frames in one launch
 WIRE_BYTES = 12  # SVO_WIRE_BYTES: the larger wire record (12 B general, 8 B compact: Tree.wire_bytes(desc))
-CEIL_K0 = 2  # SVO_CEIL_K0: the finest column-ceiling blocks are 4^2 = 16 columns wide
+CEIL_K0 = 2  # SVO_CEIL_K0 of include/svo_rt.h (the finest column-ceiling blocks are 4^k0 columns wide); the loaded library's: ceiling_layout()
 VIEW_SOLID, VIEW_ALL = 0, 1  # SVO_VIEW_*: castRayFromCam's blocks / every stored block (the shading scene)
 
 
@@ -145,7 +145,7 @@ ABI_SYMBOLS = (
     "svo_nccl_unique_id", "svo_exchange_create", "svo_exchange_wrap", "svo_exchange_destroy", "svo_exchange_info",
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
-    "svo_tree_guard_trips", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_tree_schedule", "svo_cast_ray_from_cam_async",
+    "svo_tree_guard_trips", "svo_ceiling_layout", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_tree_schedule", "svo_cast_ray_from_cam_async",
 )
 
 
@@ -163,6 +163,14 @@ def lib_sha256():
         with open(LIB_PATH, "rb") as f:
             _lib_sha = hashlib.sha256(f.read()).hexdigest()
     return _lib_sha
+
+
+def ceiling_layout():
+    """(k0, pair_step) of the loaded library (svo_ceiling_layout): the finest column-ceiling blocks are 4^k0 columns wide,
+    and the pair table pairs level j with level j + pair_step"""
+    k0, st = C.c_int32(), C.c_int32()
+    _check(lib().svo_ceiling_layout(C.byref(k0), C.byref(st)), "svo_ceiling_layout")
+    return k0.value, st.value
 
 
 def lib():
@@ -587,7 +595,7 @@ class Tree:
         out = np.zeros(n.value, np.int16)
         _check(lib().svo_tree_ceilings(self._h, out.ctypes.data_as(C.c_void_p), n.value, C.byref(lv), C.byref(n)), "svo_tree_ceilings")
         E = 1 << (2 * self.info().levels)
-        k0 = CEIL_K0  # the finest level's blocks are 4^SVO_CEIL_K0 columns wide
+        k0 = ceiling_layout()[0]  # the finest level's blocks are 4^SVO_CEIL_K0 columns wide
         assert sum((E >> (2 * (k0 + j))) ** 2 for j in range(lv.value)) == n.value
         self.ceil_k0 = k0
         res, off = [], 0

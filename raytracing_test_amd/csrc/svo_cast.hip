@@ -1854,7 +1854,11 @@ static void frame_axes(CastParams& P, int dirs) {
 // Primary casts: 16 and 64 columns (C3 0.1824 -> 0.1787 ms, C5 0.562 -> 0.543 against 64 / 256; 16 / 256 was
 // slower than both: profiles/r03/ab_j_*.log).  The shading pass walks every level (trace CEIL 2: P.ceilq); its
 // pair levels are unused.
-constexpr int kCeilPrimary[2] = {0, 1}, kCeilShade[2] = {0, 1};
+constexpr int kCeilPrimary[2] = {0, kCeilPairStep}, kCeilShade[2] = {0, kCeilPairStep};
+// (a launch's second level is read from the pair table, whose high half is level lv[0] + kCeilPairStep: the box of
+// level lv[1] must come with the ceiling of a block that holds it)
+static_assert(kCeilPrimary[1] - kCeilPrimary[0] == kCeilPairStep && kCeilShade[1] - kCeilShade[0] == kCeilPairStep,
+              "ceiling pairs: the second level must be the pair table's partner level");
 
 static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& P, const int lv[2]) {
     P.ceil = nullptr;
@@ -1862,7 +1866,9 @@ static void set_ceilings(const svo_tree* t, const svo_cast_desc* d, CastParams& 
     if (d->flags & SVO_CAST_NO_CEILINGS) return;
     P.ceil = reinterpret_cast<const int16_t*>(t->d_ceil);
     P.ceil_levels = t->ceil_levels > lv[1] ? 2 : (t->ceil_levels > lv[0] ? 1 : 0);
-    // (the pair table of level lv[0] holds lv[0] + 1 = lv[1] when the tree has it, else lv[0] itself — as below)
+    // (the pair table of level lv[0] holds lv[0] + kCeilPairStep = lv[1] when the tree has it, else its coarsest level, whose
+    // blocks hold level lv[0]'s: with one level the kernel's second box is then level lv[0]'s — as below — under a ceiling
+    // at least as high as that block's own, which is safe)
     P.ceilp = P.ceil_levels > 0 ? reinterpret_cast<const uint32_t*>(t->d_ceilp) + t->ceilp_off[lv[0]] : nullptr;
     P.ceilq = P.ceil_levels > 0 ? reinterpret_cast<const uint64_t*>(t->d_ceilq) : nullptr;
     for (int j = 0; j < 2; j++) {
@@ -2065,13 +2071,13 @@ extern "C" void svo_tree_destroy(svo_tree* t) {
     delete t;
 }
 
-// The ceiling pairs of level j (its block's ceiling, low 16 bits; its level-(j+1) block's, high; the last level paired
-// with itself) over the blocks holding columns [x0, x1) x [z0, z1) — widened to whole parent blocks, whose change reaches
+// The ceiling pairs of level j (its block's ceiling, low 16 bits; its level-(j + kCeilPairStep) block's, high, or the coarsest
+// level's when the tree has fewer) over the blocks holding columns [x0, x1) x [z0, z1) — widened to whole parent blocks, whose change reaches
 // every child's pair.  Returns per level the first and last row written (level j's rows of blocks, row-major [z][x]).
 static void ceil_pairs(svo_tree* t, int32_t n, int64_t x0, int64_t z0, int64_t x1, int64_t z1, int64_t zr[kCeilMax][2]) {
     for (int32_t j = 0; j < n; j++) {
         const int64_t rows = (int64_t)1 << (2 * (t->levels - kCeilK0 - j));
-        const int32_t up = j + 1 < n ? j + 1 : j, sh = up > j ? 2 : 0;
+        const int32_t up = std::min(j + kCeilPairStep, n - 1), sh = 2 * (up - j);
         const int32_t ush = 2 * (kCeilK0 + up), bsh = 2 * (kCeilK0 + j);
         const int64_t rows_up = rows >> sh;
         const int64_t bz0 = (z0 >> ush) << (ush - bsh), bz1 = std::min(rows, (((z1 - 1) >> ush) + 1) << (ush - bsh));
@@ -2571,6 +2577,12 @@ extern "C" int svo_tree_schedule(const svo_tree* t, void* stream, int32_t kind, 
         if (order) HIP_TRY(hipMemcpy(order, base, *n / kSchedGroup * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
         if (cost) HIP_TRY(hipMemcpy(cost, base + e.blocks, *n * sizeof(uint32_t), hipMemcpyDeviceToHost), SVO_EDEVICE);
     }
+    return SVO_OK;
+}
+
+extern "C" int svo_ceiling_layout(int32_t* k0, int32_t* pair_step) {
+    if (k0) *k0 = kCeilK0;
+    if (pair_step) *pair_step = kCeilPairStep;
     return SVO_OK;
 }
 

@@ -121,6 +121,7 @@ int32_t tree_top_y(const svo_tree* t);  // svo_world.cpp
 // in the block is empty, whatever the tree holds (overhangs included).  Level j's blocks are row-major
 // [z][x] at out[off[j] ..]; returns the number of levels.
 constexpr int32_t kCeilK0 = SVO_CEIL_K0, kCeilMax = 4;  // 16-, 64-, 256- and 1024-column blocks
+constexpr int32_t kCeilPairStep = SVO_CEIL_PAIR_STEP;    // the pair table: level j with level j + kCeilPairStep
 int32_t tree_ceilings(const svo_tree* t, std::vector<int16_t>& out, int64_t off[kCeilMax]);
 // levels 1 .. nlev-1 re-derived over the blocks holding columns [x0, x1) x [z0, z1)
 void ceilings_coarsen(const svo_tree* t, std::vector<int16_t>& out, const int64_t off[kCeilMax], int32_t nlev, int64_t x0, int64_t z0,

@@ -109,8 +109,9 @@ def test_patched_tree_casts_match_oracle(rt, oracle_mod, torch_cuda):
     assert torch_cuda.equal(a, b)
 
 
-def _pairs_of(c, E, k0, lv):
-    """the pair table the kernels read, derived from the ceilings (svo_cast.hip ceil_pairs)"""
+def _pairs_of(c, E, k0, lv, step):
+    """the pair table the kernels read, derived from the ceilings (svo_cast.hip ceil_pairs): level j with level
+    min(j + step, lv - 1)"""
     offs, o = [], 0
     for j in range(lv):
         rows = E >> (2 * (k0 + j))
@@ -119,9 +120,9 @@ def _pairs_of(c, E, k0, lv):
     p = np.zeros(len(c), np.uint32)
     for j in range(lv):
         o, rows = offs[j]
-        up = j + 1 if j + 1 < lv else j
+        up = min(j + step, lv - 1)
         ou, ru = offs[up]
-        sh = 2 if up > j else 0
+        sh = 2 * (up - j)
         lvl = c[o:o + rows * rows].reshape(rows, rows).astype(np.uint16).astype(np.uint32)
         par = c[ou:ou + ru * ru].reshape(ru, ru).astype(np.uint16).astype(np.uint32)
         p[o:o + rows * rows] = (lvl | (np.repeat(np.repeat(par, 1 << sh, 0), 1 << sh, 1) << 16)).reshape(-1)
@@ -173,8 +174,9 @@ def test_sync_updates_device_ceilings_incrementally(rt, torch_cuda):
         lv, c, p = tree.device_ceilings()
         full = np.concatenate([x.reshape(-1) for x in tree.ceilings()])
         assert lv == lv0 and np.array_equal(c, full), "step %d: device ceilings differ from a full recomputation" % step
-        assert np.array_equal(p, _pairs_of(full, E, rt.CEIL_K0, lv)), "step %d: pair table" % step
-        assert np.array_equal(tree.device_ceiling_quads(), _quads_of(full, E, rt.CEIL_K0, lv)), "step %d: quads" % step
+        k0, step_ = rt.ceiling_layout()
+        assert np.array_equal(p, _pairs_of(full, E, k0, lv, step_)), "step %d: pair table" % step
+        assert np.array_equal(tree.device_ceiling_quads(), _quads_of(full, E, k0, lv)), "step %d: quads" % step
     tree.sync()  # nothing changed: no-op
     assert np.array_equal(tree.device_ceilings()[1], c)
     print("edit + sync of 30-60 blocks: %s ms" % ", ".join("%.2f" % (x * 1e3) for x in times))
