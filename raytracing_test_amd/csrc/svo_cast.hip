@@ -745,6 +745,88 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
     return 63u - (pk & 63u);
 }
 
+// Column-ceiling march (round 5).  A descending ray above the ceiling of its 16-column block crosses, cell by cell,
+// only empty voxels until its row reaches that ceiling or it leaves the block; castRayFromCam's DDA (ray_caster.cpp:71-80)
+// takes its x / z / y steps at the crossing values T_k + j * a_k, so every event that matters here is one fma of an
+// integer index: the x (z) event entering the next block, j = the cells left in the block on that axis, and the y event
+// entering the ceiling row c, j = y - 1 - c.  The march walks the blocks the ray's column path crosses (their order
+// follows from the x / z boundary events alone) comparing exact event values, one 32-bit ceiling load per block (the
+// next block's load issued before this one is judged), until the ceiling event comes first or the ray enters a block
+// at or below its ceiling; every voxel entered before that event is then empty, and one closed-form crossing
+// (skip_box) moves the ray to the state right after it — the cell that event enters is the loop's next untested
+// voxel.  This replaces the chain of per-block ceiling moves of a ray's descent (C3: ~6 of its ~11 loop iterations,
+// each a full iteration with its own exact crossing) by one crossing and a few integer / fma steps per block.
+// Linear rays only (every sum exact: `fast` in the non-segment instances), stepping down (R.s[1] < 0); a tie between
+// the x and z boundary events (a block corner) or between a boundary and the ceiling event stops the march there.
+// Returns whether the ray moved.
+template <bool STATS, bool TRACK, bool RB>
+__device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* __restrict__ ceilp, Ray& R, uint32_t wm, bool wseg, Stats& st) {
+    const uint32_t lsh = P.ceil_sh[0];  // the finest level's blocks: 2^lsh columns
+    const uint32_t bm = (1u << lsh) - 1u, rows = (wm + 1u) >> lsh, rm = rows - 1u;
+    const int32_t wy = (int32_t)((uint32_t)R.r[1] & wm);
+    const uint32_t wx = (uint32_t)R.r[0] & wm, wz = (uint32_t)R.r[2] & wm;
+    // per axis the next block-boundary event: its index from the current state (the cells left in the block) and value
+    int32_t jx = (int32_t)(R.s[0] > 0 ? bm - (wx & bm) : (wx & bm)), jz = (int32_t)(R.s[2] > 0 ? bm - (wz & bm) : (wz & bm));
+    double Ex = on_grid(R.T[0], jx, R.a(0)), Ez = on_grid(R.T[2], jz, R.a(2));
+    uint32_t bx = wx >> lsh, bz = wz >> lsh;
+    const uint32_t dx = R.s[0] > 0 ? 1u : rm, dz = R.s[2] > 0 ? 1u : rm;  // (one block on, wrapped)
+    uint32_t cv = ceilp[__umul24(bz, rows) + bx];
+    double Ein = -__builtin_inf();  // the event that entered the current block (none for the first)
+    int32_t ein_axis = -1, ein_j = 0, stop_axis = -1, stop_j = 0;
+    for (int32_t it = 0; it < 4096; it++) {
+        const bool xn = Ex < Ez;
+        // the next block's ceiling, loaded before this block is judged (the blocks' order follows from x / z alone)
+        const uint32_t nbx = xn ? (bx + dx) & rm : bx, nbz = xn ? bz : (bz + dz) & rm;
+        const uint32_t ncv = ceilp[__umul24(nbz, rows) + nbx];
+        const int32_t jy = wy - 1 - (int32_t)(int16_t)(cv & 0xFFFFu);  // the y event entering the ceiling row
+        const double tc = jy >= 0 ? on_grid(R.T[1], jy, R.a(1)) : -__builtin_inf();
+        if (!(tc > Ein)) {  // the voxel entering this block is at or below its ceiling: end before that event
+            stop_axis = ein_axis;
+            stop_j = ein_j;
+            break;
+        }
+        const double Eexit = xn ? Ex : Ez;
+        // the next boundary lies beyond the budget: this block holds the rest of it (end before its entering event)
+        const bool far = (xn ? jx : jz) > R.steps;
+        if (!(Eexit < tc) || Ex == Ez || far) {
+            if (far) {
+                stop_axis = ein_axis;
+                stop_j = ein_j;
+            } else if (Ez <= tc && Ez <= Ex) {  // the first unproven event, in the DDA's order at ties: z, y, x
+                stop_axis = 2;
+                stop_j = jz;
+            } else if (tc <= Ex) {
+                stop_axis = 1;
+                stop_j = jy;
+            } else {
+                stop_axis = 0;
+                stop_j = jx;
+            }
+            break;
+        }
+        if (STATS) st.ceil_moves++;
+        Ein = Eexit;  // on into the next block
+        if (xn) {
+            ein_axis = 0;
+            ein_j = jx;
+            jx += (int32_t)bm + 1;
+            Ex = on_grid(R.T[0], jx, R.a(0));
+        } else {
+            ein_axis = 2;
+            ein_j = jz;
+            jz += (int32_t)bm + 1;
+            Ez = on_grid(R.T[2], jz, R.a(2));
+        }
+        bx = nbx;
+        bz = nbz;
+        cv = ncv;
+    }
+    if (stop_axis < 0) return false;  // nothing proven beyond the current voxel
+    // (selects on values: a dynamically indexed register array would go through scratch)
+    const int32_t ex[3] = {stop_axis == 0 ? stop_j : R.steps, stop_axis == 1 ? stop_j : R.steps, stop_axis == 2 ? stop_j : R.steps};
+    return skip_box<TRACK, RB>(R, ex, wseg);
+}
+
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
 // direction after them, reflection count, finalColorMod (a vec3: liquid tints per channel), and
 // whether the ray was bent.
@@ -893,6 +975,9 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     const uint32_t* const ceilp = CEIL == 3 ? P.sceilp : P.ceilp;
     uint32_t ckey = 0xFFFFFFFFu, cval = 0u;  // the lane's 16-column block (key) and its ceilings (c0 | c1 << 16)
     uint64_t cq = 0ull;                      // (CEIL 2: the ceilings of the blocks of every level holding the lane's 16-column block)
+    // the descent through the air above the terrain in one march (ceil_march): linear primary / AO rays stepping down
+    // (the voxel it ends in is untested, even when the budget ends with it: the loop tests it)
+    if (CEIL == 1 && !REFLECT && !SEG && ceil_on && !done && fast && R.s[1] < 0 && R.steps > 0) (void)ceil_march<STATS, TRACK, RB>(P, ceilp, R, wm, wseg, st);
     while (!done) {
         // the voxel just entered is untested
         if (STATS) {
