@@ -759,8 +759,11 @@ __device__ __forceinline__ uint32_t brick_walk(Ray& R, uint64_t bmask, const uin
 // Linear rays only (every sum exact: `fast` in the non-segment instances), stepping down (R.s[1] < 0); a tie between
 // the x and z boundary events (a block corner) or between a boundary and the ceiling event stops the march there.
 // Returns whether the ray moved.
-template <bool STATS, bool TRACK, bool RB>
-__device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* __restrict__ ceilp, Ray& R, uint32_t wm, bool wseg, Stats& st) {
+// The march's end: ex (skip_box's exits) of the first event whose voxel it could not prove empty.  Returns false when
+// nothing beyond the current voxel is proven (its own row is at or below its block's ceiling).
+template <bool STATS>
+__device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* __restrict__ ceilp, const Ray& R, uint32_t wm, int32_t ex[3],
+                                           Stats& st) {
     const uint32_t lsh = P.ceil_sh[0];  // the finest level's blocks: 2^lsh columns
     const uint32_t bm = (1u << lsh) - 1u, rows = (wm + 1u) >> lsh, rm = rows - 1u;
     const int32_t wy = (int32_t)((uint32_t)R.r[1] & wm);
@@ -773,31 +776,28 @@ __device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* 
     uint32_t cv = ceilp[__umul24(bz, rows) + bx];
     double Ein = -__builtin_inf();  // the event that entered the current block (none for the first)
     int32_t ein_axis = -1, ein_j = 0, stop_axis = -1, stop_j = 0;
-    for (int32_t it = 0; it < 4096; it++) {
+    for (int32_t it = 0;; it++) {
         const bool xn = Ex < Ez;
         // the next block's ceiling, loaded before this block is judged (the blocks' order follows from x / z alone)
         const uint32_t nbx = xn ? (bx + dx) & rm : bx, nbz = xn ? bz : (bz + dz) & rm;
         const uint32_t ncv = ceilp[__umul24(nbz, rows) + nbx];
         const int32_t jy = wy - 1 - (int32_t)(int16_t)(cv & 0xFFFFu);  // the y event entering the ceiling row
         const double tc = jy >= 0 ? on_grid(R.T[1], jy, R.a(1)) : -__builtin_inf();
-        if (!(tc > Ein)) {  // the voxel entering this block is at or below its ceiling: end before that event
-            stop_axis = ein_axis;
+        if (!(tc > Ein) || it == 1024) {  // the voxel entering this block is at or below its ceiling: end before that event
+            stop_axis = ein_axis;        // (and a bound on the march: its blocks so far are proven)
             stop_j = ein_j;
             break;
         }
         const double Eexit = xn ? Ex : Ez;
-        // the next boundary lies beyond the budget: this block holds the rest of it (end before its entering event)
+        // the next boundary lies beyond the budget: only the ceiling event can come first within it
         const bool far = (xn ? jx : jz) > R.steps;
         if (!(Eexit < tc) || Ex == Ez || far) {
-            if (far) {
-                stop_axis = ein_axis;
-                stop_j = ein_j;
-            } else if (Ez <= tc && Ez <= Ex) {  // the first unproven event, in the DDA's order at ties: z, y, x
-                stop_axis = 2;
-                stop_j = jz;
-            } else if (tc <= Ex) {
+            if (far || !(Ez <= tc && Ez <= Ex) && tc <= Ex) {  // the first unproven event, in the DDA's order at ties: z, y, x
                 stop_axis = 1;
                 stop_j = jy;
+            } else if (Ez <= tc && Ez <= Ex) {
+                stop_axis = 2;
+                stop_j = jz;
             } else {
                 stop_axis = 0;
                 stop_j = jx;
@@ -821,10 +821,11 @@ __device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* 
         bz = nbz;
         cv = ncv;
     }
-    if (stop_axis < 0) return false;  // nothing proven beyond the current voxel
     // (selects on values: a dynamically indexed register array would go through scratch)
-    const int32_t ex[3] = {stop_axis == 0 ? stop_j : R.steps, stop_axis == 1 ? stop_j : R.steps, stop_axis == 2 ? stop_j : R.steps};
-    return skip_box<TRACK, RB>(R, ex, wseg);
+    ex[0] = stop_axis == 0 ? stop_j : R.steps;
+    ex[1] = stop_axis == 1 ? stop_j : R.steps;
+    ex[2] = stop_axis == 2 ? stop_j : R.steps;
+    return stop_axis >= 0;
 }
 
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
@@ -977,7 +978,12 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     uint64_t cq = 0ull;                      // (CEIL 2: the ceilings of the blocks of every level holding the lane's 16-column block)
     // the descent through the air above the terrain in one march (ceil_march): linear primary / AO rays stepping down
     // (the voxel it ends in is untested, even when the budget ends with it: the loop tests it)
-    if (CEIL == 1 && !REFLECT && !SEG && ceil_on && !done && fast && R.s[1] < 0 && R.steps > 0) (void)ceil_march<STATS, TRACK, RB>(P, ceilp, R, wm, wseg, st);
+    // (primary / AO casts, and the shading pass's rays before any bounce; exact-sum lanes only: `lin` in segment instances)
+    constexpr bool MARCH = CEIL == 1 || CEIL == 2;
+    if (MARCH && ceil_on && !done && (SEG ? lin : fast) && R.s[1] < 0 && R.steps > 0) {
+        int32_t ex[3];
+        if (ceil_march<STATS>(P, ceilp, R, wm, ex, st)) (void)skip_box<TRACK, RB>(R, ex, wseg);
+    }
     while (!done) {
         // the voxel just entered is untested
         if (STATS) {
