@@ -869,7 +869,7 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
 template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, int CEIL = 0,
-          class Mem>
+          bool NO_T = false, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1,
@@ -928,7 +928,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // Instances without segments run rays from integral / half-integral origins only (need_seg):
     // every sum they take is exact, so they recover the output crossing value once at the end
     // (T - a on the last step's axis) instead of keeping it on every brick step
-    constexpr bool TRACK = REFLECT || SEG;
+    // (NO_T: no crossing value is output — shading launches without hit records — so none is kept)
+    constexpr bool TRACK = (REFLECT || SEG) && !NO_T;
     uint32_t ud[3];
     if (DIRS != 0) {
 #pragma unroll
@@ -1335,7 +1336,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             *ray_work = (unsigned long long)min(st.lookups, 65535u) | ((unsigned long long)min(st.iters, 65535u) << 16) |
                         ((unsigned long long)min(st.brick_steps, 65535u) << 32) | ((unsigned long long)min(st.loads, 65535u) << 48);
     }
-    if (!TRACK && R.axis < 3u) {
+    if (!TRACK && !NO_T && R.axis < 3u) {
         // the last step's crossing: T - a exactly (exact sums); an infinite absDelta only comes
         // with an infinite crossing (deltaPos = inf - frac * inf), which stays inf
         const double Ta = R.axis == 0u ? R.T[0] : (R.axis == 1u ? R.T[1] : R.T[2]);
@@ -1560,7 +1561,7 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
     }
 }
 
-template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0>
+template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0, bool NOREC = false>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO instances run 8 waves too (4 spilled VGPRs; with
 // the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
 // against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 5 waves without
@@ -1622,7 +1623,7 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
         // (stepsLeft 0: a miss or a hit on the last step) (uniform)
         const bool look_risk = P.look_dev ? P.look_dev[6] <= 0 : (P.look_valid && P.look_empty);
         const int32_t esc = (P.pos || look_risk) ? -1 : P.top_scene;
-        const Hit h = trace<STATS, true, true, SEG, 0, false, 2>(
+        const Hit h = trace<STATS, true, true, SEG, 0, false, 2, NOREC>(
             P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
             &bn, nullptr, esc, P.top_scene);
         shade_out<DIRS>(P, smem, path, h, bn, out);
@@ -1868,14 +1869,14 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
     }
     if (SHADE && !STATS && !wide && dirs) {  // the sun's octant (shadow rays)
         switch (dirs) {
-            case 1: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); return;
-            case 2: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); return;
-            case 3: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); return;
-            case 4: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); return;
-            case 5: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); return;
-            case 6: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); return;
-            case 7: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); return;
-            default: hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); return;
+            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, 0, st, P); return;
+            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, 0, st, P); return;
+            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, 0, st, P); return;
+            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, 0, st, P); return;
+            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, 0, st, P); return;
+            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, 0, st, P); return;
+            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, 0, st, P); return;
+            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, 0, st, P); return;
         }
     }
     if (SHADE || seg) {
