@@ -113,7 +113,10 @@ constexpr int kSchedGroup = SVO_SCHED_GROUP;  // frame schedules order groups of
 // were resolved to their measured winners and removed from the source; the losing sides are in git history
 // (DESIGN.md cites the commits) and build_variant.py --rev rebuilds them.  The critical-path diagnostics
 // (an iteration cap, dropping the top tile rows) are patches: tools/variants/*.patch, build_variant.py --patch)
-constexpr int kShadeWaves = 5;  // waves per SIMD of the shading instances: 88 VGPRs, no spills (its LDS — path + bounce state — allows 5-6; 6 waves: 80 VGPRs, 1.3 % slower; 8 with the bounce state in registers spilled 22 VGPRs: 2.5 % slower)
+// waves per SIMD of the shading instances: 80 VGPRs, no VGPR spills (its LDS — path + bounce state — allows 5-6).  With the
+// straight trace on the camera's octant (round 5) 6 waves measured 0.7 % faster than 5 (85 VGPRs); before it, 1.3 % slower
+// (profiles/r05/shade_split_ab.json); 8 with the bounce state in registers spilled 22 VGPRs: 2.5 % slower
+constexpr int kShadeWaves = 6;
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -828,6 +831,15 @@ __device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* 
     return stop_axis >= 0;
 }
 
+// A shading ray's DDA state on entering the first block it hits (the cell, crossing values, budget and last step axis):
+// the straight trace before any bounce hands it to the reflection / refraction trace, which resumes from it (trace XS)
+struct RayState {
+    double T[3];
+    int32_t r[3];
+    int32_t steps;
+    uint32_t axis;
+};
+
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
 // direction after them, reflection count, finalColorMod (a vec3: liquid tints per channel), and
 // whether the ray was bent.
@@ -869,11 +881,11 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
 template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, int CEIL = 0,
-          bool NO_T = false, class Mem>
+          bool NO_T = false, int XS = 0, class Mem>
 __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const uint16_t* mats, const Path& path, const float o[3],
                                      const float d[3], int32_t budget, unsigned long long* ray_work = nullptr,
                                      Bounce* bounce = nullptr, Parent* par_out = nullptr, int32_t top = -1, int32_t pre_top = -1,
-                                     const FrameAxes* fx = nullptr) {
+                                     const FrameAxes* fx = nullptr, RayState* xs = nullptr) {
     Ray R;
     if (DIRS != 0 && fx) {
         // a frame ray of an octant instance: the origin's part of dda_axis is the frame's (fx)
@@ -950,12 +962,25 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     par.mask = 1ull;
     par.ref = 0u;
     par.sh = 2u * (uint32_t)P.levels;
+    // XS 2: resume a ray from the state its straight trace (XS 1) stopped in — the cell it entered, untested; the
+    // flags above (fast, lin: from the origin and direction) are the ones that trace had
     bool done = R.steps <= 0;
-    if (!done) dda_step(R);
+    if (XS == 2) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            R.T[k] = xs->T[k];
+            R.r[k] = xs->r[k];
+        }
+        R.steps = xs->steps;
+        R.axis = xs->axis;
+        done = false;
+    } else if (!done) {
+        dda_step(R);
+    }
     // pre_top (>= 0: the tree's highest stored voxel row, tree_top_y): a ray starting above it is in
     // one empty region {y > pre_top} (every x, z; up to the wrap in y) and crosses it in one move,
     // exactly like a box (false: its budget ends up there, state unchanged, the loop walks it)
-    if (pre_top >= 0 && fast && !done) {
+    if (XS != 2 && pre_top >= 0 && fast && !done) {
         uint32_t w[3];
         wrap3(R, wm, w);
         if ((int32_t)w[1] > pre_top) {
@@ -981,7 +1006,7 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     // (the voxel it ends in is untested, even when the budget ends with it: the loop tests it)
     // (primary / AO casts, and the shading pass's rays before any bounce; exact-sum lanes only: `lin` in segment instances)
     constexpr bool MARCH = CEIL == 1 || CEIL == 2;
-    if (MARCH && ceil_on && !done && (SEG ? lin : fast) && R.s[1] < 0 && R.steps > 0) {
+    if (XS != 2 && MARCH && ceil_on && !done && (SEG ? lin : fast) && R.s[1] < 0 && R.steps > 0) {
         int32_t ex[3];
         if (ceil_march<STATS>(P, ceilp, R, wm, ex, st)) (void)skip_box<TRACK, RB>(R, ex, wseg);
     }
@@ -1301,6 +1326,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         }
     }
     if (par_out) *par_out = par;
+    if (XS == 1 && hit) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            xs->T[k] = R.T[k];
+            xs->r[k] = R.r[k];
+        }
+        xs->steps = R.steps;
+        xs->axis = R.axis;
+    }
     if (STATS) {
         // SIMD efficiency: a lane's work units (lookups + voxel steps) against the wave's maximum
         const uint32_t work = st.lookups + st.brick_steps + st.plain_steps;
@@ -1517,7 +1551,8 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
                 // shadow ray towards the sun from the centre of lastPos, through empty and liquid
                 const float so[3] = {(float)(h.x - (ax == 0u ? sg : 0)) + 0.5f, (float)(h.y - (ax == 1u ? sg : 0)) + 0.5f,
                                      (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
-                // (DIRS of a shading instance: the sun's step octant — every shadow ray steps with it)
+                // (DIRS: a sign octant every shadow ray of the launch steps with; shading launches pass 0 — their instances are
+                // specialised on the camera's octant instead, k_cast)
                 dark = (trace<false, false, true, false, DIRS, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                             .info & HIT_BIT) != 0u;
             }
@@ -1564,7 +1599,7 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
 template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0, bool NOREC = false>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO instances run 8 waves too (4 spilled VGPRs; with
 // the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
-// against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 5 waves without
+// against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 6 waves without VGPR
 // spills (kShadeWaves)
 __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
@@ -1623,10 +1658,26 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
         // (stepsLeft 0: a miss or a hit on the last step) (uniform)
         const bool look_risk = P.look_dev ? P.look_dev[6] <= 0 : (P.look_valid && P.look_empty);
         const int32_t esc = (P.pos || look_risk) ? -1 : P.top_scene;
-        const Hit h = trace<STATS, true, true, SEG, 0, false, 2, NOREC>(
-            P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
-            &bn, nullptr, esc, P.top_scene);
-        shade_out<DIRS>(P, smem, path, h, bn, out);
+        unsigned long long* const rw = P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr;
+        if (STATS || STAMPS) {  // (diagnostics: one trace, bounces included)
+            const Hit h = trace<STATS, true, true, SEG, 0, false, 2, NOREC>(P, mem, P.mats, path, o, d, P.steps, rw, &bn, nullptr, esc, P.top_scene);
+            shade_out<0>(P, smem, path, h, bn, out);
+        } else {
+            // the straight trace to the first block hit — no reflection / refraction upkeep per step, on the camera's step
+            // octant (DIRS) — and only a mirror or a refractive block with budget left hands its state on to the bouncing
+            // trace, which resumes there (shaded C3 0.3103 -> 0.3027 ms, then 0.2914 with the octant; the straight trace's
+            // state on its first hit is the one the bouncing trace from the origin reaches: both take castRayFromCam's
+            // exact steps).  Its column ceilings: the launch's two levels (CEIL 1, as primary casts: 0.8 % faster than the walk
+            // over every level, CEIL 2, which the bouncing trace keeps)
+            RayState xs;
+            Hit h = trace<false, false, true, SEG, DIRS, false, 1, NOREC, 1>(P, mem, P.mats, path, o, d, P.steps, nullptr, nullptr, nullptr,
+                                                                             esc, P.top_scene, DIRS != 0 ? &P.fax[frm] : nullptr, &xs);
+            const uint32_t mf = ((h.info & HIT_BIT) && h.steps_left > 0) ? P.mat_flags[h.info & MAT_MASK] & 7u : 0u;
+            if (mf == 3u || mf == 5u)
+                h = trace<false, true, true, SEG, 0, false, 2, NOREC, 2>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, esc,
+                                                                     P.top_scene, nullptr, &xs);
+            shade_out<0>(P, smem, path, h, bn, out);
+        }
     } else if (out >= 0) {
         Parent pfin;
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO, 1>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
@@ -1867,7 +1918,7 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
         else launch_dirs<AO, false>(dirs, grid, block, st, P);
         return;
     }
-    if (SHADE && !STATS && !wide && dirs) {  // the sun's octant (shadow rays)
+    if (SHADE && !STATS && !wide && dirs) {  // the camera's octant (the straight trace of the shading rays)
         switch (dirs) {
             case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, 0, st, P); return;
             case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, 0, st, P); return;
@@ -2468,18 +2519,19 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     HIP_TRY(hipSetDevice(t->device), SVO_EDEVICE);
     const int64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks * kBlock > 0xFFFFFFFFll) SVO_FAIL(SVO_ERANGE, "svo_shade_rays: too many rays for one launch");
-    // shadow rays all step with the sun's signs (an exact zero component: generic flags)
-    int sun_dirs = (P.flags & SVO_CAST_NO_OCTANT) ? 0 : 1;
-    for (int k = 0; k < 3 && sun_dirs; k++) {
-        if (P.sun[k] < 0.0f) sun_dirs += 1 << k;
-        else if (!(P.sun[k] > 0.0f)) sun_dirs = 0;
-    }
     const bool wide = wide_nodes(t, d->flags) || wide_nodes(sc, d->flags);
     std::unique_lock<std::mutex> sched_lock;  // (held from here until the launch and the sort are queued)
     const SchedUse sch = sched_attach(t, d, P, 2, blocks, (hipStream_t)stream, sched_lock);
     if (P.flags & SVO_CAST_STATS) launch_cast<true, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
     else if (P.flags & SVO_CAST_TIMELINE) launch_cast<false, true, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P);
-    else launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, sun_dirs);
+    else {
+        // the straight trace runs on the camera's step octant (frame launches whose every pixel steps with it: frame_dirs;
+        // shaded C3 0.3050 -> 0.2914 ms against generic sign flags, with the shadow rays' sun-octant instances given up
+        // for it: profiles/r05/shade_split_ab.json)
+        const int dirs = frame_dirs(P);
+        frame_axes(P, dirs);
+        launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, dirs);
+    }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return sched_order(t, sch, (hipStream_t)stream);
 }

@@ -1,0 +1,8 @@
+#!/bin/bash
+# r05_v: shading rays trace straight to their first hit, and only mirrors / refractive blocks with budget left resume
+# in the bouncing trace (split) — shading parity, A/B shaded C3
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_v; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_split.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_shade.py tests/test_gpu_schedule.py tests/test_gpu_bridge.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=3 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_v_sh variants/libsvo_norec2.so variants/libsvo_split.so || exit 1
