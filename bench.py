@@ -388,7 +388,7 @@ def launch_ranks(n, argv, grace_s=30.0, script=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS),
                     help="c3: depth-12 / 1080p (the metric); c5: depth-14 / 4K; c2: the reference world / 1080p / S=300 from the "

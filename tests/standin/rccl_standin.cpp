@@ -293,8 +293,9 @@ STANDIN_API ncclResult_t ncclCommInitRank(ncclComm_t* out, int nranks, ncclUniqu
 
 STANDIN_API ncclResult_t ncclCommDestroy(ncclComm_t c) {
     if (!c) return ncclInvalidArgument;
-    // this rank's announcement and any message addressed to it that nobody received; the last rank out removes the directory
-    unlink((c->dir + "/rank" + std::to_string(c->rank)).c_str());
+    // any message addressed to this rank that nobody received; then it marks itself gone (its announcement stays: a rank
+    // still in ncclCommInitRank's barrier must find it — ranks with nothing to exchange may finish before a slow one has
+    // joined), and the last rank out removes the announcements and the directory
     if (DIR* d = opendir(c->dir.c_str())) {
         while (struct dirent* e = readdir(d)) {
             int src = -1, dst = -1;
@@ -303,7 +304,17 @@ STANDIN_API ncclResult_t ncclCommDestroy(ncclComm_t c) {
         }
         closedir(d);
     }
-    rmdir(c->dir.c_str());  // (fails while another rank is still in; that rank removes it)
+    const int fd = open((c->dir + "/left" + std::to_string(c->rank)).c_str(), O_CREAT | O_WRONLY, 0600);
+    if (fd >= 0) close(fd);
+    bool last = true;
+    for (int r = 0; r < c->nranks && last; r++) last = access((c->dir + "/left" + std::to_string(r)).c_str(), F_OK) == 0;
+    if (last) {
+        for (int r = 0; r < c->nranks; r++) {
+            unlink((c->dir + "/rank" + std::to_string(r)).c_str());
+            unlink((c->dir + "/left" + std::to_string(r)).c_str());
+        }
+        rmdir(c->dir.c_str());
+    }
     delete c;
     return ncclSuccess;
 }

@@ -31,6 +31,8 @@ RANK_SCRIPT = textwrap.dedent(r'''
         while not os.path.exists(idfile):
             time.sleep(0.01)
         ctypes.memmove(ctypes.byref(uid), open(idfile, "rb").read(), 128)
+    if mode == "late" and me == N - 1:
+        time.sleep(2.0)  # joins after the others have finished and left
     comm = ctypes.c_void_p()
     rc = lib.ncclCommInitRank(ctypes.byref(comm), N, uid, me)
     assert rc == 0, rc
@@ -73,6 +75,8 @@ RANK_SCRIPT = textwrap.dedent(r'''
             rc = lib.ncclRecv(buf, ctypes.c_size_t(8), U8, 0, comm, None)
             assert rc == 5, rc  # ncclInvalidUsage
         print("ok mismatch", me)
+    elif mode == "late":
+        print("ok late", me)
     elif mode == "timeout":
         if me == 1:
             buf = ctypes.create_string_buffer(8)
@@ -117,3 +121,11 @@ def test_standin_size_mismatch_is_an_error(standin, tmp_path):
 
 def test_standin_receive_times_out(standin, tmp_path):
     _ranks(standin, tmp_path, 2, "timeout", timeout_s="1")
+
+
+def test_standin_rank_joining_after_the_others_left(standin, tmp_path):
+    """ranks with nothing to exchange may finish and destroy their communicator before a slow rank has passed
+    ncclCommInitRank's barrier (seen under a loaded CPU suite): their announcements stay until the last rank is out"""
+    outs = _ranks(standin, tmp_path, 3, "late")
+    assert all("ok late" in o for o, _ in outs)
+    assert [p for p in os.listdir(tmp_path) if p.startswith("svo_rccl_standin_")] == []
