@@ -158,3 +158,22 @@ def test_world_size_must_match_gpus(monkeypatch):
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], capture_output=True, text=True, env=env,
                        timeout=120)
     assert p.returncode == 2 and "differs from --gpus" in p.stderr
+
+
+def test_product_build_is_a_noop_when_up_to_date(monkeypatch, tmp_path):
+    """build() compiles nothing when libsvo_rt.so is newer than every source and header, even without its objects
+    (gpurun snapshots leave *.o behind: the GPU box must time the library the PMC passes measured)"""
+    from raytracing_test_amd import build as b
+
+    b.build()  # (up to date, or brought up to date here)
+    calls = []
+    monkeypatch.setattr(b, "_run", lambda cmd: calls.append(cmd))
+    monkeypatch.setattr(b, "BUILD", str(tmp_path / "no_objects"))  # as on the box: no objects at all
+    assert b.build() == b.OUT and calls == []
+    # a source newer than the library does rebuild (into the object directory it is given)
+    src = os.path.join(os.path.dirname(b.__file__), "csrc", "svo_exchange.hip")
+    st = os.stat(b.OUT)
+    real = os.path.getmtime
+    monkeypatch.setattr(os.path, "getmtime", lambda p: st.st_mtime + 10 if p == src else (real(p) if os.path.exists(p) else 0.0))
+    b.build()
+    assert any("svo_exchange.hip" in " ".join(c) for c in calls)
