@@ -349,6 +349,18 @@ cat $OUT/smoke.log
 bash tools/evidence.sh ${R05_FINAL_TAG:-r05_final}/ev || exit $?
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final>}
+r05_ab() {
+# r05_ab: the record index taken again after the trace (rec: primary instances without spills) and the primary
+# instances at 7 waves (w7, 66 VGPRs, no spills) against the HEAD build (h9f) — full GPU suite on rec, A/B C3 / C4 / C5
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ab; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_rec.so timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 bash tools/ab_lib.sh r05_ab_c3 variants/libsvo_h9f.so variants/libsvo_rec.so variants/libsvo_w7.so || exit 1
+REPS=2 BENCH_ARGS="--ao 16" bash tools/ab_lib.sh r05_ab_ao variants/libsvo_h9f.so variants/libsvo_rec.so variants/libsvo_w7.so || exit 1
+REPS=2 BENCH_ARGS="--config c5" bash tools/ab_lib.sh r05_ab_c5 variants/libsvo_h9f.so variants/libsvo_rec.so variants/libsvo_w7.so || exit 1
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
