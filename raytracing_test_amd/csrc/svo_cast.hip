@@ -878,6 +878,10 @@ __device__ __forceinline__ void refract_dir(float d[3], const float nin[3]) {
 // DIRS (1..8): every ray of the launch steps with the signs dirs_sign(DIRS, k) (frame_dirs proves it
 // on the host): the steps are compile-time constants and the sign branches of the crossings and brick
 // walks fold away; 0: per-wave sign flags (dir_flags)
+// NO_T: no crossing value is output (shading launches without hit records), so none is tracked per step.
+// XS (round 5, the shading pass): 1 — on a hit, store the DDA state the ray entered its block with in *xs (RayState);
+// 2 — start from *xs instead of the origin's first step (the flags fast / lin still from the origin and direction),
+// with no pre-top box and no march: the straight trace of a shading ray hands its first hit on to the bouncing one
 __host__ __device__ constexpr int32_t dirs_sign(int DIRS, int k) { return DIRS == 0 ? 0 : (((DIRS - 1) >> k) & 1) ? -1 : 1; }
 
 template <bool STATS, bool REFLECT = false, bool ESCAPE = false, bool SEG = false, int DIRS = 0, bool KEEPPAR = false, int CEIL = 0,

@@ -361,6 +361,15 @@ REPS=2 BENCH_ARGS="--ao 16" bash tools/ab_lib.sh r05_ab_ao variants/libsvo_h9f.s
 REPS=2 BENCH_ARGS="--config c5" bash tools/ab_lib.sh r05_ab_c5 variants/libsvo_h9f.so variants/libsvo_rec.so variants/libsvo_w7.so || exit 1
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab>}
+r05_ac() {
+# r05_ac: shadow rays with wave-uniform sign flags in scalar registers (uni) — shading parity, A/B shaded C3 vs h9f
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ac; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_uni.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_shade.py tests/test_gpu_schedule.py tests/test_gpu_bridge.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ac_sh variants/libsvo_h9f.so variants/libsvo_uni.so || exit 1
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
