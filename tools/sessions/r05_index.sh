@@ -370,6 +370,22 @@ rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep
 REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ac_sh variants/libsvo_h9f.so variants/libsvo_uni.so || exit 1
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac>}
+r05_ad() {
+# r05_ad: where the shaded frame's time goes on the split build (tools/shade_parts.py), and the frame schedule on / off
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ad; mkdir -p $OUT
+timeout -k 10 300 python tools/shade_parts.py > $OUT/shade_parts.txt 2>&1 || { tail $OUT/shade_parts.txt; exit 1; }
+cat $OUT/shade_parts.txt
+for rep in 1 2 3; do
+timeout -k 10 120 python bench.py --shade --no-cpu-baseline --steps 30 > $OUT/sched_on_$rep.json 2>/dev/null || exit 1
+timeout -k 10 120 python bench.py --shade --no-cpu-baseline --steps 30 --cast-flags 65536 > $OUT/sched_off_$rep.json 2>/dev/null || exit 1
+done
+python3 -c "
+import json
+for m in ('on','off'):
+    print('schedule', m, [json.loads([l for l in open('$OUT/sched_%s_%d.json'%(m,r)) if l.startswith('{')][-1])['ms_per_step'] for r in (1,2,3)])"
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
