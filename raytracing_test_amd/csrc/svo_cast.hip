@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
                                                                              esc, P.top_scene, DIRS != 0 ? &P.fax[frm] : nullptr, &xs);
             const uint32_t mf = ((h.info & HIT_BIT) && h.steps_left > 0) ? P.mat_flags[h.info & MAT_MASK] & 7u : 0u;
             if (mf == 3u || mf == 5u)
-                h = trace<false, true, true, SEG, 0, false, 2, NOREC, 2>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, esc,
+                h = trace<false, true, true, true, 0, false, 2, NOREC, 2>(P, mem, P.mats, path, o, d, P.steps, nullptr, &bn, nullptr, esc,
                                                                      P.top_scene, nullptr, &xs);
             shade_out<0>(P, smem, path, h, bn, out);
         }
@@ -1922,16 +1922,18 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
         else launch_dirs<AO, false>(dirs, grid, block, st, P);
         return;
     }
-    if (SHADE && !STATS && !wide && dirs) {  // the camera's octant (the straight trace of the shading rays)
+    // the camera's octant (the straight trace of the shading rays); without hit records, a launch whose every origin is
+    // exact (seg: need_seg false) takes the straight trace without segment bounds (the bouncing trace keeps them)
+    if (SHADE && !STATS && !wide && dirs) {
         switch (dirs) {
-            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, 0, st, P); return;
-            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, 0, st, P); return;
-            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, 0, st, P); return;
-            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, 0, st, P); return;
-            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, 0, st, P); return;
-            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, 0, st, P); return;
-            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, 0, st, P); return;
-            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, 0, st, P); return;
+            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 1, true>), grid, block, 0, st, P); return;
+            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 2, true>), grid, block, 0, st, P); return;
+            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 3, true>), grid, block, 0, st, P); return;
+            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 4, true>), grid, block, 0, st, P); return;
+            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 5, true>), grid, block, 0, st, P); return;
+            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 6, true>), grid, block, 0, st, P); return;
+            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 7, true>), grid, block, 0, st, P); return;
+            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 8, true>), grid, block, 0, st, P); return;
         }
     }
     if (SHADE || seg) {
@@ -2531,10 +2533,10 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     else {
         // the straight trace runs on the camera's step octant (frame launches whose every pixel steps with it: frame_dirs;
         // shaded C3 0.3050 -> 0.2914 ms against generic sign flags, with the shadow rays' sun-octant instances given up
-        // for it: profiles/r05/shade_split_ab.json)
+        // for it: profiles/r05/shade_split_ab.json); its segment bounds only when an origin needs them (0.2887 -> 0.2831)
         const int dirs = frame_dirs(P);
         frame_axes(P, dirs);
-        launch_cast<false, false, false, true>(wide, true, dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, dirs);
+        launch_cast<false, false, false, true>(wide, need_seg(P), dim3((uint32_t)blocks), dim3(kBlock), (hipStream_t)stream, P, dirs);
     }
     HIP_TRY(hipGetLastError(), SVO_EDEVICE);
     return sched_order(t, sch, (hipStream_t)stream);

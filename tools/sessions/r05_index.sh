@@ -386,6 +386,33 @@ for m in ('on','off'):
     print('schedule', m, [json.loads([l for l in open('$OUT/sched_%s_%d.json'%(m,r)) if l.startswith('{')][-1])['ms_per_step'] for r in (1,2,3)])"
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad>}
+r05_ae() {
+# r05_ae: the shading pass's straight trace without segment bounds when every origin is exact (seg0: need_seg) — shading
+# parity, A/B shaded C3 against the final build (h18 = 18957fa5)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ae; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_seg0.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_shade.py tests/test_gpu_schedule.py tests/test_gpu_bridge.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ae_sh variants/libsvo_h18.so variants/libsvo_seg0.so || exit 1
+}
+
+r05_final3() {
+# r05_final3: the final build (the straight shading trace without segment bounds for exact origins): the GPU suite,
+# smoke, every config's PMC passes (copied into this box's profiles/ so the bench lines read them), then tools/evidence.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_final3; mkdir -p $OUT; export TMPDIR=/tmp
+sha256sum raytracing_test_amd/libsvo_rt.so
+echo "[r05_final3] $(date +%T) pytest"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+bash tools/pmc_all.sh r05_pmc3 || exit $?
+for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc3_$k/pmc_summary.json profiles/pmc_$k.json || exit 1; done
+bash tools/evidence.sh r05_final3/ev || exit $?
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
