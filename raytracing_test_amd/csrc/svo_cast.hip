@@ -113,10 +113,12 @@ constexpr int kSchedGroup = SVO_SCHED_GROUP;  // frame schedules order groups of
 // were resolved to their measured winners and removed from the source; the losing sides are in git history
 // (DESIGN.md cites the commits) and build_variant.py --rev rebuilds them.  The critical-path diagnostics
 // (an iteration cap, dropping the top tile rows) are patches: tools/variants/*.patch, build_variant.py --patch)
-// waves per SIMD of the shading instances: 80 VGPRs, no VGPR spills (its LDS — path + bounce state — allows 5-6).  With the
-// straight trace on the camera's octant (round 5) 6 waves measured 0.7 % faster than 5 (85 VGPRs); before it, 1.3 % slower
-// (profiles/r05/shade_split_ab.json); 8 with the bounce state in registers spilled 22 VGPRs: 2.5 % slower
-constexpr int kShadeWaves = 6;
+// waves per SIMD of the shading instances on the camera's octant: 72 VGPRs (0-4 spilled).  The LDS allows 7 blocks per
+// SIMD when the launch's path depth is its own (dynamic, path_lds: 3.75 KB for 6 levels) and the bounce state packs into
+// 28 B per lane: 7 waves measured 4 % faster than 6 (80 VGPRs), which was 0.7 % faster than 5 (85 VGPRs) with the straight
+// trace on the camera's octant (profiles/r05/shade_split_ab.json); 8 with the bounce state in registers spilled 22 VGPRs.
+// The generic-sign instance (no octant) runs 6 (80 VGPRs: 7 would spill 29)
+constexpr int kShadeWaves = 7;
 constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
 
 struct Hit {
@@ -842,12 +844,13 @@ struct RayState {
 
 // Reflections and refractions of the shading pass (reflectRay / refractRay, low_res.frag:170-240):
 // direction after them, reflection count, finalColorMod (a vec3: liquid tints per channel), and
-// whether the ray was bent.
+// whether the ray was bent (kBent, a bit of the reflection count's word: 28 B per lane in LDS, which with the launch's own
+// path depth lets the shading instances run 7 waves per SIMD).
+constexpr int32_t kBent = 1 << 30;
 struct Bounce {
     float d[3];
-    int32_t n;
+    int32_t n;  // reflections | kBent
     float m[3];
-    bool bent;
 };
 
 // refractRay(vec3, vec3, float, float) (low_res.frag:196-209), n1 = 1.0, n2 = 1.1; dot as
@@ -1212,8 +1215,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             bounce->m[2] *= t2;
             uint32_t wr[3];
             wrap3(R, wm, wr);  // the refractive voxel (its region, when uniform, is passed below)
-            if (!bounce->bent) {
-                bounce->bent = true;
+            if (!(bounce->n & kBent)) {
+                bounce->n |= kBent;
                 if (STATS) st.bends++;
                 const uint32_t ax = R.axis;
                 double ex[3];
@@ -1548,7 +1551,7 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
         const float inten = fminf(fmaxf(0.0f, l) + 0.4f + (facing ? 0.15f : 0.0f), 1.0f);
         c = make_float3(col.x * inten * m[0], col.y * inten * m[1], col.z * inten * m[2]);
         bool dark = false;
-        if (bn.n == 0) {
+        if ((bn.n & ~kBent) == 0) {  // (not reflected)
             if (!facing) {
                 dark = true;
             } else {
@@ -1603,9 +1606,9 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
 template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int DIRS = 0, bool NOREC = false>
 // primary rays: 64 VGPRs = 8 waves per SIMD without spills; the AO instances run 8 waves too (4 spilled VGPRs; with
 // the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
-// against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 6 waves without VGPR
-// spills (kShadeWaves)
-__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void k_cast(const CastParams P) {
+// against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 7 waves on the camera's
+// octant (kShadeWaves), 6 with generic signs
+__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWaves : 6) : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1615,7 +1618,8 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
     const unsigned long long t_start = (STAMPS || sched) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     // per-lane node path (mask and first-child index of the interior node at each depth of the
     // last descent), [depth][lane]
-    __shared__ uint32_t path_words[(kMaxLevels - 1) * 3 * kBlock];
+    // (dynamic LDS: the launch's own depth, path_lds — a 6-level tree's shading launch fits 7 blocks per SIMD)
+    extern __shared__ uint32_t path_words[];
     const Path path = {path_words + threadIdx.x};
     // (the hemisphere AO sample set is read from the kernel arguments: uniform loads, no LDS)
     __shared__ Bounce shade_bn[SHADE ? kBlock : 1];  // shading: the rays' bounce state (k_cast SHADE below)
@@ -1655,7 +1659,7 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? kShadeWaves : 8)) void
         // the ray's bounce state lives in LDS: the trace touches it only at reflections / refractions, and in registers
         // it cost the loop spills (22 VGPRs at 8 waves; 0.4748 -> 0.4660 ms per shaded C3 frame at 5 waves without them)
         Bounce& bn = shade_bn[threadIdx.x];
-        bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}, false};
+        bn = {{d[0], d[1], d[2]}, 0, {1.0f, 1.0f, 1.0f}};
         // rays may escape (stop early once only empty voxels lie ahead) unless their end position is output (hit records)
         // or could be the highlighted lookingAtBlock (low_res.frag:347 compares every ray's end, misses too): a look-at
         // voxel the scene may not store — the host's, checked on the host, or a device pick record that is not a sure hit
@@ -1900,19 +1904,22 @@ static int ao_plan_get(const svo_tree* t, int32_t n, int32_t steps, const float*
 // buffer offset reaches (or on request)
 bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap >= kNarrowNodes || (flags & SVO_CAST_WIDE_ADDR); }
 
+// The per-lane LDS path of k_cast (Path): 3 dwords per interior depth (levels - 1 of them) per lane of the block
+size_t path_lds(const CastParams& P) { return (size_t)(P.levels > 1 ? P.levels - 1 : 1) * 3 * kBlock * sizeof(uint32_t); }
+
 // seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always);
 // dirs: frame_dirs (the plain primary instance of narrow trees has one per sign octant)
 template <bool AO, bool SEG>
 void launch_dirs(int dirs, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
     switch (dirs) {
-        case 1: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 1>), grid, block, 0, st, P); return;
-        case 2: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 2>), grid, block, 0, st, P); return;
-        case 3: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 3>), grid, block, 0, st, P); return;
-        case 4: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 4>), grid, block, 0, st, P); return;
-        case 5: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 5>), grid, block, 0, st, P); return;
-        case 6: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 6>), grid, block, 0, st, P); return;
-        case 7: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 7>), grid, block, 0, st, P); return;
-        default: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 8>), grid, block, 0, st, P); return;
+        case 1: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 1>), grid, block, path_lds(P), st, P); return;
+        case 2: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 2>), grid, block, path_lds(P), st, P); return;
+        case 3: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 3>), grid, block, path_lds(P), st, P); return;
+        case 4: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 4>), grid, block, path_lds(P), st, P); return;
+        case 5: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 5>), grid, block, path_lds(P), st, P); return;
+        case 6: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 6>), grid, block, path_lds(P), st, P); return;
+        case 7: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 7>), grid, block, path_lds(P), st, P); return;
+        default: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 8>), grid, block, path_lds(P), st, P); return;
     }
 }
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
@@ -1926,22 +1933,22 @@ void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, con
     // exact (seg: need_seg false) takes the straight trace without segment bounds (the bouncing trace keeps them)
     if (SHADE && !STATS && !wide && dirs) {
         switch (dirs) {
-            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 1, true>), grid, block, 0, st, P); return;
-            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 2, true>), grid, block, 0, st, P); return;
-            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 3, true>), grid, block, 0, st, P); return;
-            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 4, true>), grid, block, 0, st, P); return;
-            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 5, true>), grid, block, 0, st, P); return;
-            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 6, true>), grid, block, 0, st, P); return;
-            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 7, true>), grid, block, 0, st, P); return;
-            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, 0, st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, 0, st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 8, true>), grid, block, 0, st, P); return;
+            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 1, true>), grid, block, path_lds(P), st, P); return;
+            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 2, true>), grid, block, path_lds(P), st, P); return;
+            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 3, true>), grid, block, path_lds(P), st, P); return;
+            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 4, true>), grid, block, path_lds(P), st, P); return;
+            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 5, true>), grid, block, path_lds(P), st, P); return;
+            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 6, true>), grid, block, path_lds(P), st, P); return;
+            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 7, true>), grid, block, path_lds(P), st, P); return;
+            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 8, true>), grid, block, path_lds(P), st, P); return;
         }
     }
     if (SHADE || seg) {
-        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, 0, st, P);
-        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false, true>), grid, block, 0, st, P);
+        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, path_lds(P), st, P);
+        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, false, true>), grid, block, path_lds(P), st, P);
     } else {
-        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, true, false>), grid, block, 0, st, P);
-        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, false, false>), grid, block, 0, st, P);
+        if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, true, false>), grid, block, path_lds(P), st, P);
+        else hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, false, false, false>), grid, block, path_lds(P), st, P);
     }
 }
 

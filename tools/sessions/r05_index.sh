@@ -413,6 +413,26 @@ for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc3_$k/pmc_summary
 bash tools/evidence.sh r05_final3/ev || exit $?
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3>}
+r05_af() {
+# r05_af: DIAGNOSTIC (levels-6 trees only: a 5-level LDS path) — the shading kernel at 7 waves (72 VGPRs, the bent flag
+# packed into the reflection count, LDS 5.6 KB per block) against the final build (de28): shaded C3 timing only
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_af_sh variants/libsvo_de28.so variants/libsvo_s7.so || exit 1
+}
+
+r05_ag() {
+# r05_ag: the shading kernel at 7 waves for real (the launch's own LDS path depth, the bent flag packed: s7b = the
+# product build) — the full GPU suite on it, A/B shaded C3 / C3 / C4 / C5 against de28 (the previous final build)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ag; mkdir -p $OUT
+timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ag_sh variants/libsvo_de28.so variants/libsvo_s7b.so || exit 1
+REPS=3 bash tools/ab_lib.sh r05_ag_c3 variants/libsvo_de28.so variants/libsvo_s7b.so || exit 1
+REPS=2 BENCH_ARGS="--ao 16" bash tools/ab_lib.sh r05_ag_ao variants/libsvo_de28.so variants/libsvo_s7b.so || exit 1
+REPS=2 BENCH_ARGS="--config c5" bash tools/ab_lib.sh r05_ag_c5 variants/libsvo_de28.so variants/libsvo_s7b.so || exit 1
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
