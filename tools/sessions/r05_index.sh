@@ -450,6 +450,19 @@ for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc4_$k/pmc_summary
 bash tools/evidence.sh r05_final4/ev || exit $?
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4>}
+r05_ah() {
+# r05_ah: the first-dispatched tile rows cast by half footprints (32 rays per wave): SVO_HALF_ROWS 0 (the final build's
+# layout) / 4 / 8 / 16 — parity of the primary casts on h8, A/B C3 / C4 / C5 / shaded
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ah; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_h8.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_configs.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=3 bash tools/ab_lib.sh r05_ah_c3 variants/libsvo_h0.so variants/libsvo_h4.so variants/libsvo_h8.so variants/libsvo_h16.so || exit 1
+REPS=2 BENCH_ARGS="--config c5" bash tools/ab_lib.sh r05_ah_c5 variants/libsvo_h0.so variants/libsvo_h4.so variants/libsvo_h8.so variants/libsvo_h16.so || exit 1
+REPS=2 BENCH_ARGS="--ao 16" bash tools/ab_lib.sh r05_ah_ao variants/libsvo_h0.so variants/libsvo_h4.so variants/libsvo_h8.so variants/libsvo_h16.so || exit 1
+REPS=2 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ah_sh variants/libsvo_h0.so variants/libsvo_h4.so variants/libsvo_h8.so variants/libsvo_h16.so || exit 1
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
