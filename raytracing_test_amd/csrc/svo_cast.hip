@@ -2118,6 +2118,9 @@ constexpr size_t kSchedMax = 16;  // schedules per tree (least recently used rep
 // 0.308 -> 0.358 when a stale order was used — a wrong order is worse than the default one.  A frame far from the last
 // one is not sorted after either (the sort costs ~9 us): the schedule comes back one frame after the camera settles.
 constexpr float kSchedTurnCos = 0.99996f;  // cos(0.5 deg)
+// A still camera's order holds for the next frames too: a scheduled frame writes its durations and is sorted after only
+// every kSchedEvery-th frame (the sort, one workgroup for ~9 us between two launches, is otherwise on every frame's path)
+constexpr int32_t kSchedEvery = 4;
 constexpr float kSchedMove = 1.0f;
 struct SchedUse {  // a launch's schedule (sched_attach), by value: the tree's list may change under other threads
     uint32_t* base = nullptr;
@@ -2144,7 +2147,8 @@ SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, 
             (void)hipFree(lru->d_buf);  // (synchronises the device: no launch still reads it)
             t->scheds.erase(lru);
         }
-        t->scheds.push_back(svo_tree::Sched{(void*)st, kind, {0}, 0, nullptr, 0, false, {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}});
+        t->scheds.push_back(svo_tree::Sched{(void*)st, kind, {0}, 0, nullptr, 0, false, 0, {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f},
+                                            {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}});
         s = &t->scheds.back();
     }
     s->last_use = ++t->sched_clock;
@@ -2164,18 +2168,30 @@ SchedUse sched_attach(const svo_tree* t, const svo_cast_desc* d, CastParams& P, 
         s->primed = false;
     }
     const float cam[6] = {P.frame_org[0], P.frame_org[1], P.frame_org[2], d->cam_dir[0], d->cam_dir[1], d->cam_dir[2]};
-    const float dx = cam[0] - s->cam[0], dy = cam[1] - s->cam[1], dz = cam[2] - s->cam[2];
-    const float cs = cam[3] * s->cam[3] + cam[4] * s->cam[4] + cam[5] * s->cam[5];
-    const bool near = dx * dx + dy * dy + dz * dz <= kSchedMove * kSchedMove && cs >= kSchedTurnCos;
-    std::copy(cam, cam + 6, s->cam);
+    const auto close = [&](const float* c) {
+        const float dx = cam[0] - c[0], dy = cam[1] - c[1], dz = cam[2] - c[2];
+        return dx * dx + dy * dy + dz * dz <= kSchedMove * kSchedMove && cam[3] * c[3] + cam[4] * c[4] + cam[5] * c[5] >= kSchedTurnCos;
+    };
+    const bool near_last = close(s->last_cam);            // (a frame far from the last one is not sorted after)
+    const bool near_sorted = s->primed && close(s->cam);  // (the order is used only near the frame it was sorted from)
+    std::copy(cam, cam + 6, s->last_cam);
     uint32_t* base = reinterpret_cast<uint32_t*>(s->d_buf);
-    P.sched_order = s->primed && near ? base : nullptr;
-    P.sched_cost = base + blocks;
-    if (!near) {  // (a moving camera: no sort after this frame; the first frame near it sorts for the next)
+    P.sched_order = near_sorted ? base : nullptr;
+    if (!near_last) {  // (a moving camera: no sort after this frame; the first frame near it sorts for the next)
+        P.sched_cost = nullptr;
         s->primed = false;
         return SchedUse{nullptr, blocks, kind};
     }
-    return SchedUse{base, blocks, kind};
+    // sorted after this frame: an order missing or sorted from a camera this one has drifted from, else every
+    // kSchedEvery-th frame.  Only the frames sorted after write their durations, so the stored order is always the sort of
+    // the stored durations (svo_tree_schedule)
+    const bool sort = !near_sorted || ++s->since >= kSchedEvery;
+    if (sort) {
+        s->since = 0;
+        std::copy(cam, cam + 6, s->cam);
+    }
+    P.sched_cost = sort ? base + blocks : nullptr;
+    return SchedUse{sort ? base : nullptr, blocks, kind};
 }
 // after the launch of a scheduled frame: the next frame's order (the schedule counts as sorted once the sort is queued);
 // called with sched_attach's lock still held

@@ -103,7 +103,9 @@ struct svo_tree {
         void* d_buf;
         uint64_t last_use;
         bool primed;  // order holds a sorted schedule (else: the frame runs in the natural order and writes costs)
+        int32_t since;  // scheduled frames since the last sort (a sort every kSchedEvery frames)
         float cam[6];  // the camera (origin of the launch's first frame, direction) of the frame whose durations it holds
+        float last_cam[6];  // the camera of the last frame on this schedule
     };
     mutable std::vector<Sched> scheds;
     mutable std::mutex sched_mu;

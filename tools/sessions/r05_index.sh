@@ -463,6 +463,30 @@ REPS=2 BENCH_ARGS="--ao 16" bash tools/ab_lib.sh r05_ah_ao variants/libsvo_h0.so
 REPS=2 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ah_sh variants/libsvo_h0.so variants/libsvo_h4.so variants/libsvo_h8.so variants/libsvo_h16.so || exit 1
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah>}
+r05_ai() {
+# r05_ai: the frame schedule sorted every 4th scheduled frame (se4) against the final build (ae = aedae530) — the
+# schedule and shading suites on se4, A/B shaded C3
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ai; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_se4.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_schedule.py tests/test_gpu_shade.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_ai_sh variants/libsvo_ae.so variants/libsvo_se4.so || exit 1
+}
+
+r05_aj() {
+# r05_aj: the frame schedule sorted every 4th frame and used only near the camera it was sorted from (se4b) against the
+# final build (ae) — schedule / shading suites on se4b, A/B shaded C3, and both under camera motion (tools/shade_motion.py)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_aj; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_se4b.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_schedule.py tests/test_gpu_shade.py > $OUT/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc: $(tail -1 $OUT/pytest.log)"; [ $rc -ne 0 ] && { grep -E "^E |FAILED" $OUT/pytest.log | head -20; exit $rc; }
+REPS=4 BENCH_ARGS="--shade" bash tools/ab_lib.sh r05_aj_sh variants/libsvo_ae.so variants/libsvo_se4b.so || exit 1
+for v in ae se4b; do
+SVO_LIB=$PWD/variants/libsvo_$v.so timeout -k 10 300 python tools/shade_motion.py > $OUT/motion_$v.txt 2>&1 || { tail $OUT/motion_$v.txt; exit 1; }
+echo "== $v"; tail -8 $OUT/motion_$v.txt
+done
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
