@@ -179,10 +179,10 @@ int svo_tree_device_ceilings(const svo_tree* t, int16_t* ceil, uint32_t* pairs, 
    level j in bits 16j..16j+15 (a level the tree lacks: 0x7FFF).  quads may be NULL (count only); n = elements. */
 int svo_tree_device_ceiling_quads(const svo_tree* t, uint64_t* quads, int64_t cap, int64_t* n);
 /* The frame schedule of (hip_stream, kind: 2 shading; 0 / 1, primary and AO casts, keep none) over t (inspection /
-   tests; SVO_CAST_NO_SCHEDULE): the dispatch order of the next frame of that geometry, by groups of SVO_SCHED_GROUP
-   consecutive blocks (order[slot group] = frame group; n / SVO_SCHED_GROUP entries) and the last frame's block
-   durations (100 MHz ticks, n entries); n = blocks (0: no schedule yet).  Either buffer may be NULL; synchronises
-   hip_stream. */
+   tests; SVO_CAST_NO_SCHEDULE): the dispatch order of the next frames of that geometry, by groups of SVO_SCHED_GROUP
+   consecutive blocks (order[slot group] = frame group; n / SVO_SCHED_GROUP entries) and the block durations of the frame
+   it was sorted from (100 MHz ticks, n entries); n = blocks (0: no schedule yet).  Either buffer may be NULL;
+   synchronises hip_stream. */
 int svo_tree_schedule(const svo_tree* t, void* hip_stream, int32_t kind, uint32_t* order, uint32_t* cost, int64_t cap, int64_t* n);
 /* Checkpoint (the reference regenerates its world at every start, main.cpp:190): write the
    linearised tree (levels, view, palette, nodes, material runs; a checksum) to `path`, and read it back
@@ -288,9 +288,10 @@ typedef struct {
    the tree instead */
 #define SVO_CAST_NO_CEILINGS 32768
 /* svo_cast_desc.flags, scheduling (results identical): shaded frames (svo_shade_rays) of more than
-   SVO_SCHED_MIN_BLOCKS blocks are dispatched longest block first, by the block durations the last frame of the same
-   geometry measured on the same stream (frame-to-frame coherence; a small sort kernel after each launch orders the
-   next); the first frame of a geometry runs in the default order.  This bit keeps the default order (and leaves the
+   SVO_SCHED_MIN_BLOCKS blocks are dispatched longest block first, by the block durations a recent frame of the same
+   geometry measured on the same stream (frame-to-frame coherence; a small sort kernel after every 4th frame orders the
+   next ones, used while the camera stays within 0.5 deg / 1 voxel of the frame sorted); the first frame of a geometry
+   runs in the default order.  This bit keeps the default order (and leaves the
    schedule untouched).  Primary casts always run in the default order (their longest waves are its first) */
 #define SVO_CAST_NO_SCHEDULE 65536
 #define SVO_SCHED_MIN_BLOCKS 4096
