@@ -487,6 +487,23 @@ echo "== $v"; tail -8 $OUT/motion_$v.txt
 done
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj>}
+r05_final5() {
+# r05_final5: the final build (the schedule sorted every 4th frame): the GPU suite,
+# smoke, every config's PMC passes (copied into this box's profiles/ so the bench lines read them), then tools/evidence.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_final5; mkdir -p $OUT; export TMPDIR=/tmp
+sha256sum raytracing_test_amd/libsvo_rt.so
+echo "[r05_final5] $(date +%T) pytest"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+bash tools/pmc_all.sh r05_pmc5 || exit $?
+for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc5_$k/pmc_summary.json profiles/pmc_$k.json || exit 1; done
+bash tools/evidence.sh r05_final5/ev || exit $?
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
