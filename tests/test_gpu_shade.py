@@ -255,6 +255,25 @@ def test_shade_liquid_depth12_sampled(rt, oracle_mod, torch_cuda):
         assert torch_cuda.equal(hits[k], hits2[k]), k
 
 
+def test_shade_liquid_depth14_sampled(rt, oracle_mod, torch_cuda):
+    """a 7-level tree (depth 14, the deepest the builders take: the shading kernel's LDS path is sized by the launch's
+    depth, path_lds) over 1024^2 terrain columns with lakes: sampled pixels against the oracle, and the image without
+    hit records (the no-record instances: escape, no crossing value, the straight trace without segment bounds) equal
+    to the one with them"""
+    W, H = 960, 540
+    tree = rt.Tree.terrain_gpu(7, 1024, 1024, 0)
+    scene = rt.Tree.terrain_gpu(7, 1024, 1024, 0, view=rt.VIEW_ALL)
+    org, cam_dir = (4.0, 90.0, 4.0), rt.normalize((1.0, -0.45, 1.0))
+    rgba, hits = tree.shade_frame(org, cam_dir, W, H, 16384, sun=rt.sun_dir(), with_hits=True, scene=scene, time=0.5)
+    ot = oracle_mod.Tree.terrain(7, 1024, 1024)
+    pix = np.random.default_rng(14).choice(W * H, 3000, replace=False)
+    ref = ot.shade_frame(org, cam_dir, W, H, 16384, rt.sun_dir(), pixels=pix, liquid=True, time=0.5)
+    g = rt.decode_hits(hits)
+    _check(rgba[torch_cuda.as_tensor(pix, device=rgba.device)], ref, g["hit"][pix], "depth14 lakes")
+    rgba2 = tree.shade_frame(org, cam_dir, W, H, 16384, sun=rt.sun_dir(), scene=scene, time=0.5)
+    assert torch_cuda.equal(rgba, rgba2)
+
+
 def test_full_view_tree_is_not_castable(rt, lake_scene):
     """castRayFromCam semantics need the solid view: a full-view tree is refused, not silently cast"""
     with pytest.raises(RuntimeError):
