@@ -269,7 +269,9 @@ typedef struct {
    per-face voxel plan (A/B reference path) */
 #define SVO_CAST_AO_TRACE 128
 /* svo_cast_desc.flags, scheduling (results identical): in frame mode each wavefront (one block)
-   covers 16x4 pixels of its 8-pixel tile row; these bits select 8x8 or 32x2 instead */
+   covers 16x4 pixels of its 8-pixel tile row; these bits select 8x8 or 32x2 instead.  A small launch (a
+   strong-scaling shard: whole footprints would make fewer than 20480 wavefronts) casts its first-dispatched tile rows
+   by half footprints, 32 pixels per wavefront; svo_cast_blocks counts those wavefronts too */
 #define SVO_CAST_TILE_8X8 256
 #define SVO_CAST_TILE_32X2 512
 /* svo_cast_desc.flags (results identical): read nodes through 64-bit addresses even when the tree is

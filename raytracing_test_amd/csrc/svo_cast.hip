@@ -53,6 +53,7 @@ struct CastParams {
     float sdir[3];
     int32_t width, height, tiles_x, tile_row_start, tile_row_step, tile_rows_local;
     int32_t tile_lh;  // log2 of a wavefront's pixel rows (frame_wave_lh)
+    int32_t half_rows;  // the first tile rows dispatched, cast by half footprints (frame_half_rows: small launches)
     int32_t n_frames;        // frames in this launch (>= 1); frame f casts from frame_org[3f..]
     int64_t frame_records;   // records of one frame (this shard)
     float frame_org[3 * SVO_MAX_FRAMES];
@@ -1578,19 +1579,33 @@ __device__ __forceinline__ void frame_pixel(const CastParams& P, int64_t blk, fl
     const uint32_t fr = wv % (uint32_t)P.n_frames, tile = wv / (uint32_t)P.n_frames;
     frm = fr;
     const int32_t lane = (int32_t)(threadIdx.x & 63u);
-    const uint32_t tq = tile / (uint32_t)P.tiles_x;
+    // (small launches: the first half_rows tile rows dispatched are cast by half footprints — two adjacent waves of 32
+    // lanes per footprint, 2^(lh-1) pixel rows each; frame_half_rows)
+    const uint32_t h2 = (uint32_t)P.half_rows * 2u * (uint32_t)P.tiles_x;
+    uint32_t tq, tx_;
+    int32_t half = -1;
+    if (tile < h2) {
+        tq = tile / (2u * (uint32_t)P.tiles_x);
+        const uint32_t t2 = tile - tq * 2u * (uint32_t)P.tiles_x;
+        tx_ = t2 >> 1;
+        half = (int32_t)(t2 & 1u);
+    } else {
+        const uint32_t t = tile - h2 + (uint32_t)P.half_rows * (uint32_t)P.tiles_x;
+        tq = t / (uint32_t)P.tiles_x;
+        tx_ = t - tq * (uint32_t)P.tiles_x;
+    }
     int32_t trl = (int32_t)tq;
     // default order: top tile rows first (rays nearest the horizon travel furthest; dispatching
     // them first keeps the long tiles out of the launch's tail)
     if (!(P.flags & SVO_CAST_BOTTOM_FIRST)) trl = P.tile_rows_local - 1 - trl;
-    const int32_t tx = (int32_t)(tile - tq * (uint32_t)P.tiles_x);
+    const int32_t tx = (int32_t)tx_;
     const int32_t tr = P.tile_row_start + trl * P.tile_row_step;
     // the wavefront's 2^(6-lh) x 2^lh pixels of its 8-pixel tile row (lh = 3: an 8x8 tile); the
     // sub-rows of one column of footprints are adjacent waves
     const int32_t lh = P.tile_lh, lw = 6 - lh, sub = 3 - lh;
-    const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (lane >> lw);
+    const int32_t rr = ((tx & ((1 << sub) - 1)) << lh) + (half >= 0 ? (half << (lh - 1)) : 0) + (lane >> lw);
     const int32_t px = ((tx >> sub) << lw) + (lane & ((1 << lw) - 1)), py = tr * 8 + rr;
-    if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height) {
+    if (trl >= 0 && trl < P.tile_rows_local && px < P.width && py < P.height && !(half >= 0 && lane >= 32)) {
         raygen_pixel(P.rg, px, py, d);
         o[0] = P.frame_org[3 * fr + 0];
         o[1] = P.frame_org[3 * fr + 1];
@@ -2090,15 +2105,16 @@ int fill_params(const svo_tree* t, const svo_cast_desc* d, const svo_hits* o, Ca
     if (d->n_frames < 0 || d->n_frames > SVO_MAX_FRAMES) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: n_frames outside [0, SVO_MAX_FRAMES]");
     if (d->n_frames > 1 && !d->frame_origins) SVO_FAIL(SVO_EINVAL, "svo_cast_rays: n_frames > 1 without frame_origins");
     P.n_frames = d->n_frames > 1 ? d->n_frames : 1;
+    P.half_rows = frame_half_rows(P.tile_rows_local, d->flags, P.tile_lh, P.tiles_x, P.n_frames);
     for (int32_t f = 0; f < P.n_frames; f++)
         for (int k = 0; k < 3; k++) P.frame_org[3 * f + k] = d->n_frames > 1 ? d->frame_origins[3 * f + k] : d->origin[k];
     int64_t per_frame = 0;
     for (int32_t r = d->tile_row_start; r < tile_rows; r += d->tile_row_step) per_frame += std::min(8, d->height - r * 8);
     P.frame_records = per_frame * d->width;
     // (a dispatch holds fewer than 2^32 work-items: the HSA packet's grid size is 32-bit)
-    if ((int64_t)P.tile_rows_local * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
+    if ((int64_t)(P.tile_rows_local + P.half_rows) * P.tiles_x * P.n_frames >= (int64_t)1 << 26)
         SVO_FAIL(SVO_ERANGE, "svo_cast_rays: frame too large (2^26 wavefronts or more in one launch)");
-    nthreads = (int64_t)P.tile_rows_local * P.tiles_x * P.n_frames * 64;
+    nthreads = (int64_t)(P.tile_rows_local + P.half_rows) * P.tiles_x * P.n_frames * 64;
     return SVO_OK;
 }
 

@@ -61,6 +61,19 @@ SVO_HD uint32_t child_slot(uint32_t x, uint32_t y, uint32_t z, uint32_t sh) {
 // 8-pixel tile row
 SVO_HD int32_t frame_wave_lh(int32_t flags) { return (flags & 512) ? 1 : ((flags & 256) ? 3 : 2); }
 SVO_HD int32_t frame_wave_cols(int32_t width, int32_t lh) { return ((width + (1 << (6 - lh)) - 1) >> (6 - lh)) << (3 - lh); }
+// Small launches (a strong-scaling shard: a few thousand waves, fewer than the GPU's wave slots) are bound by their
+// longest waves, the far field's: their first-dispatched (top) tile rows are cast by half footprints, 32 rays per
+// wavefront (lanes 32-63 idle), which serialise fewer diverging paths per wave.  As many rows as keep the launch within
+// kHalfWaves wavefronts; a launch already above it (a whole frame: 32400 at 1080p) keeps whole footprints, which share
+// their node reads (half footprints made full frames 3-12 % slower).  Measured, one GPU, the slowest 1/8 shard
+// (tools/shard_curve.py): C3 128.6 -> 114.2 us, C5 125.2 -> 113.6 us (ranks within 1.12x), 1/4 C3 128.3 -> 112.4
+// (profiles/r05/shard_half_footprints.json).  None bottom-first.
+constexpr int32_t kHalfWaves = 20480;
+SVO_HD int32_t frame_half_rows(int32_t rows, int32_t flags, int32_t lh, int32_t cols, int32_t frames) {
+    if ((flags & 4) || lh < 1 || rows <= 0 || cols <= 0) return 0;  // (4: SVO_CAST_BOTTOM_FIRST)
+    const int64_t k = (int64_t)kHalfWaves / ((int64_t)cols * (frames > 1 ? frames : 1)) - rows;
+    return k <= 0 ? 0 : (int32_t)(k < rows ? k : rows);
+}
 
 // hit-record info word (see include/svo_rt.h)
 enum : uint32_t { HIT_BIT = 1u << 31, AXIS_SHIFT = 16, NEG_BIT = 1u << 18, MAT_MASK = 0xFFFFu };

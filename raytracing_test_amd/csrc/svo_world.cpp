@@ -1498,7 +1498,8 @@ extern "C" int svo_cast_blocks(const svo_cast_desc* d, int64_t* n) {
     if (rc) return rc;
     const int32_t tile_rows = (d->height + 7) / 8;
     const int64_t rows = d->tile_row_start < tile_rows ? (tile_rows - d->tile_row_start + d->tile_row_step - 1) / d->tile_row_step : 0;
-    *n = rows * svo::frame_wave_cols(d->width, svo::frame_wave_lh(d->flags)) * nf;
+    const int32_t lh = svo::frame_wave_lh(d->flags), cols = svo::frame_wave_cols(d->width, lh);
+    *n = (rows + svo::frame_half_rows((int32_t)rows, d->flags, lh, cols, nf)) * cols * nf;
     return SVO_OK;
 }
 

@@ -64,7 +64,8 @@ def test_shaded_frames_identical_under_schedule(worlds, torch_cuda):
     for rep in range(3):
         assert np.array_equal(_shade(worlds, cams[0], 1280, 720, stream=s), ref), "720p frame %d" % rep
     order, cost = solid.schedule(rt.SCHED_SHADE, stream=s)
-    assert len(order) == 1280 * 720 // 64 // rt.SCHED_GROUP
+    # (720p, 14400 wavefronts of whole footprints: a small launch, its first tile rows in half footprints — svo_cast_blocks)
+    assert len(order) * rt.SCHED_GROUP == solid.blocks(solid.frame_desc(ORG, rt.normalize(cams[0]), 1280, 720, S)) > 1280 * 720 // 64
     _check_schedule(order, cost, "shading 720p")
 
 
@@ -75,10 +76,13 @@ def test_small_frames_and_primary_casts_keep_no_schedule(worlds, torch_cuda):
     assert np.array_equal(_shade(worlds, (1.0, -0.45, 1.0), 256, 256, stream=s), ref)
     assert 256 * 256 // 64 <= rt.SCHED_MIN_BLOCKS
     assert solid.schedule(rt.SCHED_SHADE, stream=s) == (None, None)
-    # 1000 x 1000: 15625 blocks, not a multiple of the schedule's groups
-    ref = _shade(worlds, (1.0, -0.45, 1.0), 1000, 1000, flags=rt.CAST_NO_SCHEDULE, stream=s)
+    # 1040 x 800: 20410 blocks (100 tile rows of 130 footprints, 57 of them in half footprints), not a multiple of the
+    # schedule's groups
+    nb = solid.blocks(solid.frame_desc(ORG, rt.normalize((1.0, -0.45, 1.0)), 1040, 800, S))
+    assert nb > rt.SCHED_MIN_BLOCKS and nb % rt.SCHED_GROUP != 0
+    ref = _shade(worlds, (1.0, -0.45, 1.0), 1040, 800, flags=rt.CAST_NO_SCHEDULE, stream=s)
     for rep in range(2):
-        assert np.array_equal(_shade(worlds, (1.0, -0.45, 1.0), 1000, 1000, stream=s), ref)
+        assert np.array_equal(_shade(worlds, (1.0, -0.45, 1.0), 1040, 800, stream=s), ref)
     assert solid.schedule(rt.SCHED_SHADE, stream=s) == (None, None)
     for ao in (0, 16):
         solid.cast_frame(ORG, rt.normalize((1.0, -0.45, 1.0)), W, H, S, stream=s, ao_samples=ao)

@@ -178,15 +178,24 @@ def test_cast_count_sharding(rt):
 
 def test_cast_blocks_per_footprint(rt):
     """blocks (64-lane wavefronts) per launch: one per 16x4 footprint by default, 8x8 / 32x2 by flag,
-    one per 64 explicit rays; every block covers at most 64 rays"""
-    for W, H in ((1920, 1080), (33, 17), (8, 8), (100, 60)):
-        for step in (1, 3):
+    one per 64 explicit rays; every block covers at most 64 rays.  A small launch (below 20480 wavefronts of whole
+    footprints: svo_common.h frame_half_rows) adds one wavefront per footprint of its first tile rows (half footprints)
+    — as many rows as keep it within 20480 — and none bottom-first"""
+    for W, H in ((1920, 1080), (3840, 2160), (33, 17), (8, 8), (100, 60)):
+        for step in (1, 2, 3, 8):
             for start in range(step):
                 tile_rows = len(range(start, (H + 7) // 8, step))
-                for flags, tw in ((0, 16), (rt.CAST_TILE_8X8, 8), (rt.CAST_TILE_32X2, 32)):
+                for flags, tw in ((0, 16), (rt.CAST_TILE_8X8, 8), (rt.CAST_TILE_32X2, 32), (rt.CAST_BOTTOM_FIRST, 16)):
                     d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], W, H, 1, tile_row_start=start, tile_row_step=step, flags=flags)
-                    assert rt.Tree.blocks(d) == tile_rows * (8 * tw // 64) * ((W + tw - 1) // tw)
+                    cols = (8 * tw // 64) * ((W + tw - 1) // tw)
+                    half = 0 if flags == rt.CAST_BOTTOM_FIRST else max(0, min(tile_rows, 20480 // cols - tile_rows))
+                    assert rt.Tree.blocks(d) == (tile_rows + half) * cols, (W, H, step, start, flags)
                     assert rt.Tree.blocks(d) * 64 >= rt.Tree.count(d)
+    # a whole 1080p frame keeps whole footprints; its 1/8 shard is all half footprints
+    d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 1920, 1080, 1)
+    assert rt.Tree.blocks(d) == 135 * 240
+    d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 1920, 1080, 1, tile_row_start=0, tile_row_step=8)
+    assert rt.Tree.blocks(d) == 2 * 17 * 240
     d = rt.Tree.frame_desc([0, 0, 0], [1, 0, 0], 8, 8, 1)
     d.ray_dirs, d.n_rays = 1, 130  # explicit mode: only the count is read
     assert rt.Tree.blocks(d) == 3

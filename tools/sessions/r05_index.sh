@@ -535,6 +535,45 @@ timeout -k 10 300 python tools/shade_parts.py > $OUT/shade_parts.txt 2>&1 || { t
 cat $OUT/shade_parts.txt
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am>}
+r05_an() {
+# r05_an: half footprints (32 rays per wave) for the first SVO_HALF_ROWS local tile rows of launches with tile_row_step
+# >= 4 only (strong-scaling shards; full frames unchanged): sh8 / sh16 / sh1000 (every row) — a verified 4-rank gloo
+# strong run on sh1000, then the one-GPU shard curves at N = 4 / 8 for the product build and each variant
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_an; mkdir -p $OUT
+SVO_LIB=$PWD/variants/libsvo_sh1000.so timeout -k 10 300 python bench.py --gpus 4 --dist-backend gloo --frames 1 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/g4.json 2> $OUT/g4.err || { tail -20 $OUT/g4.err; exit 1; }
+grep '^{' $OUT/g4.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('g4 strong verified', d.get('gather_verified'))"
+for v in default sh8 sh16 sh1000; do
+  if [ $v = default ]; then unset SVO_LIB; else export SVO_LIB=$PWD/variants/libsvo_$v.so; fi
+  for c in c3 c5; do
+    timeout -k 10 300 python tools/shard_curve.py --config $c --ns 1,4,8 --reps 15 > $OUT/shard_${c}_$v.json 2> $OUT/shard_${c}_$v.err || { tail $OUT/shard_${c}_$v.err; exit 1; }
+    python3 -c "
+import json
+d=json.loads([l for l in open('$OUT/shard_${c}_$v.json') if l.startswith('{')][-1])
+for e in d['curve']: print('$v', '$c', e['n'], e['max_us'], [round(x,1) for x in e['rank_us']])"
+  done
+done
+}
+
+r05_ao() {
+# r05_ao: the product build with half footprints for small launches (a wave budget: strong-scaling shards) — the full GPU
+# suite, the shard curves (C3 / C5, N = 1, 2, 4, 8), the C3 bench line
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ao; mkdir -p $OUT
+sha256sum raytracing_test_amd/libsvo_rt.so
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc: $(tail -1 $OUT/pytest_gpu.log)"; [ $rc -eq 0 ] || { grep -E "^E |FAILED" $OUT/pytest_gpu.log | head -20; exit $rc; }
+for c in c3 c5; do
+  timeout -k 10 300 python tools/shard_curve.py --config $c --ns 1,2,4,8 > $OUT/shard_$c.json 2> $OUT/shard_$c.err || { tail $OUT/shard_$c.err; exit 1; }
+  python3 -c "
+import json
+d=json.loads([l for l in open('$OUT/shard_$c.json') if l.startswith('{')][-1])
+for e in d['curve']: print('$c', e['n'], e['max_us'], e['ideal_us'], e.get('inflight_max_us'), [round(x,1) for x in e['rank_us']])"
+done
+timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/c3.json 2> $OUT/c3.err || exit 1
+grep '^{' $OUT/c3.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
