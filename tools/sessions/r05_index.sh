@@ -574,6 +574,23 @@ timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/c3.json 2> $OUT/c3.er
 grep '^{' $OUT/c3.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3', d['ms_per_step'], d['roofline']['avg_launch_ms'])"
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao>}
+r05_final6() {
+# r05_final6: the final build (half footprints for small launches): the GPU suite,
+# smoke, every config's PMC passes (copied into this box's profiles/ so the bench lines read them), then tools/evidence.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_final6; mkdir -p $OUT; export TMPDIR=/tmp
+sha256sum raytracing_test_amd/libsvo_rt.so
+echo "[r05_final6] $(date +%T) pytest"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -2 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
+cat $OUT/smoke.log
+bash tools/pmc_all.sh r05_pmc6 || exit $?
+for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc6_$k/pmc_summary.json profiles/pmc_$k.json || exit 1; done
+bash tools/evidence.sh r05_final6/ev || exit $?
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
