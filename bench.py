@@ -768,8 +768,9 @@ def main():
                    "ao_samples": args.ao, "shade": args.shade, "frames_per_step": nframes, "rays_per_step": W * H * nframes,
                    "parallelism": "tile-row shard x%d" % world, "launches_per_step": 1, "frames_in_flight": args.inflight, "gather": gather,
                    "dispatch_order": ("top tile rows first" if not args.shade or (flags & rt.CAST_NO_SCHEDULE) or tree.blocks(desc) <= rt.SCHED_MIN_BLOCKS else
-                                      "longest first by the last frame's block durations, in groups of 4 blocks (frame schedule, "
-                                      "gated on camera motion; the warmup's first two frames: top tile rows first)"),
+                                      "longest first by a recent frame's block durations (sorted after every 4th frame), in groups of "
+                                      "4 blocks (frame schedule, gated on camera motion; the warmup's first two frames: top tile rows "
+                                      "first)"),
                    "exchange": None if not gather else (
                        ("svo_cast_wire + svo_exchange_wire (C ABI, RCCL send/recv group): %d-B wire records written by the cast "
                         "kernel" % tree.wire_bytes(desc) + (" + AO counts" if args.ao else "") +
