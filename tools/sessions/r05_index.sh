@@ -591,6 +591,15 @@ for k in c3 c3f c3_ao16 c5 c3_shade c2; do cp gpurun_out/r05_pmc6_$k/pmc_summary
 bash tools/evidence.sh r05_final6/ev || exit $?
 }
 
-name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6>}
+r05_ap() {
+# r05_ap: the default bench line and the shaded one with the round's last bench.py (sanity)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/r05_ap; mkdir -p $OUT
+timeout -k 10 300 python bench.py > $OUT/c3.json 2> $OUT/c3.err || { tail $OUT/c3.err; exit 1; }
+timeout -k 10 300 python bench.py --shade --no-cpu-baseline > $OUT/shade.json 2> $OUT/shade.err || { tail $OUT/shade.err; exit 1; }
+for n in c3 shade; do grep '^{' $OUT/$n.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('$n', d['ms_per_step'], r.get('avg_launch_ms'), r.get('counters','')[:60], d['config'].get('dispatch_order','')[:90])"; done
+}
+
+name=${1:?usage: r05_index.sh <session name: a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6 ap>}
 shift
-case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6 " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
+case " a b c d e f g h i j k l m n o p q r s t u v w x y z aa pmc final ab ac ad ae final3 af ag final4 ah ai aj final5 ak al am an ao final6 ap " in *" $name "*) "r05_$name" "$@" ;; *) echo "no session r05_$name" >&2; exit 2 ;; esac
