@@ -37,6 +37,7 @@ Extra objects on the JSON line:
                  (rank 0, N=1), plus config C1 (dense grid) every time.
 """
 import argparse
+import collections
 import json
 import os
 import sys
@@ -330,6 +331,74 @@ def roofline(args, cfg, rays_per_launch, avg_kernel_s, world, lib_sha):
     return roof
 
 
+# ------------------------------------------------------------------------------- watchdog --
+WATCHDOG_RC = 124  # a rank's exit status when its watchdog fires (the status `timeout` gives)
+
+
+class Watchdog:
+    """N > 1: a per-rank guard against a step that never finishes (a receive whose message never comes — a stuck RCCL
+    group — leaves every rank waiting, and no rank would ever exit, so launch_ranks' / torchrun's failure handling
+    would never fire).  The main thread names its phase as it goes (`phase`: the step and cast / exchange / sync);
+    `arm(seconds, what)` sets a deadline.  When one passes, the rank writes which step and phase it is stuck in, the
+    state of its last steps' GPU events (cast done / exchange pending, queried with a bounded wait), and every
+    thread's Python traceback (faulthandler) to stderr, and leaves with WATCHDOG_RC through os._exit — no re-exec;
+    the launcher then ends the other ranks."""
+
+    def __init__(self, rank, world):
+        import threading
+
+        self.rank, self.world = rank, world
+        self.phase = "start"
+        self.deadline = None
+        self.what = ""
+        self.bound = 0.0
+        self.diag = None  # () -> str: the GPU events of the last steps (bench main)
+        self.t = threading.Thread(target=self._run, name="bench-watchdog", daemon=True)
+        self.t.start()
+
+    def arm(self, seconds, what):
+        self.bound = float(seconds)
+        self.what = what
+        self.deadline = time.monotonic() + self.bound
+
+    def disarm(self):
+        self.deadline = None
+
+    def _run(self):
+        while True:
+            time.sleep(0.1)
+            dl = self.deadline
+            if dl is not None and time.monotonic() > dl:
+                self._fire()
+
+    def _fire(self):
+        import faulthandler
+        import threading
+
+        err = sys.stderr
+        err.write("bench.py: rank %d of %d: WATCHDOG: %s did not finish within %.1f s; stuck in phase: %s\n"
+                  % (self.rank, self.world, self.what, self.bound, self.phase))
+        err.flush()
+        faulthandler.dump_traceback(file=err, all_threads=True)
+        err.flush()
+        if self.diag is not None:  # (a GPU query could block behind a runtime lock the stuck call holds: bounded)
+            out = []
+            th = threading.Thread(target=lambda: out.append(self.diag()), daemon=True)
+            th.start()
+            th.join(3.0)
+            err.write("bench.py: rank %d: GPU events of the last steps: %s\n" % (self.rank, out[0] if out else "(query did not return)"))
+        err.flush()
+        os._exit(WATCHDOG_RC)
+
+
+def watchdog_bound(warm_s, warm_steps, steps):
+    """The timed region's bound from the warm-up's wall time per step (which includes the first launches' and the
+    communicator's set-up, so it overestimates a step): SVO_WATCHDOG_FACTOR (default 20) times the steps' expected time,
+    at least SVO_WATCHDOG_MIN_S (default 60 s)"""
+    per = warm_s / max(1, warm_steps)
+    return max(float(os.environ.get("SVO_WATCHDOG_MIN_S", "60")), float(os.environ.get("SVO_WATCHDOG_FACTOR", "20")) * per * (steps + 2))
+
+
 # ------------------------------------------------------------------------------ rank launcher --
 def _free_port():
     import socket
@@ -456,6 +525,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(args.dist_backend)
+    wd = Watchdog(rank, world) if world > 1 else None
+    if wd:  # (set-up: the tree build, buffers, the communicator)
+        wd.arm(float(os.environ.get("SVO_WATCHDOG_SETUP_S", "600")), "set-up (tree build, exchange communicator)")
     cfg = dict(CONFIGS[args.config])
     if args.cols is not None:
         cfg["cols"] = args.cols
@@ -525,7 +597,8 @@ def main():
     xmode = None
     # the C-ABI exchange needs RCCL; a gloo rehearsal takes it too when SVO_RCCL_LIB names the test-only stand-in
     # (tests/standin/rccl_standin.cpp: several ranks on one GPU, host-staged), else the torch exchange
-    standin = os.environ.get("SVO_RCCL_LIB") or None
+    # (the library honours SVO_RCCL_LIB only with SVO_RCCL_STANDIN=1 as well)
+    standin = (os.environ.get("SVO_RCCL_LIB") or None) if os.environ.get("SVO_RCCL_STANDIN") == "1" else None
     if gather:
         xmode = "torch" if (args.shade or args.exchange == "torch" or (args.dist_backend != "nccl" and not standin)) else "capi"
     # tensors for the small control collectives: on the GPU over RCCL, on the host over gloo
@@ -596,10 +669,22 @@ def main():
                            outs, nbuf)
 
     xdone = [None] * nbuf
-    cast_done = [torch.cuda.Event() for _ in range(nbuf)]
+    # N > 1: the last steps' cast / exchange events (the watchdog's report; per-step events, not per buffer set)
+    recent = collections.deque(maxlen=6)
+
+    def events_state():
+        def st(e):
+            return "-" if e is None else ("done" if e.query() else "PENDING")
+        return "; ".join("step %d: cast %s, exchange %s" % (k, st(c), st(x)) for k, c, x in list(recent)) or "(no step issued)"
+
+    if wd:
+        wd.diag = events_state
+
     def one_step(k, ev=None, pipe=False):
         b = k % nbuf
         stream = cstreams[k % 2] if pipe else cstreams[0]
+        if wd:
+            wd.phase = "step %d: cast (svo_cast%s)" % (k, "_wire" if wires is not None else "_rays")
         with torch.cuda.stream(stream):
             if xdone[b] is not None:
                 stream.wait_event(xdone[b])  # the exchange that read this buffer set has passed
@@ -614,31 +699,52 @@ def main():
                 tree.cast(desc, outs[b], stream)
             if ev is not None:
                 ev[1].record(stream)
+        ce = None
+        if wd or xmode == "capi":
+            ce = torch.cuda.Event()
+            ce.record(stream)
         if not gather:
+            if wd:
+                recent.append((k, ce, None))
             return
+        if wd:
+            wd.phase = "step %d: exchange (%s)" % (k, "svo_exchange_wire: RCCL send / recv group, decode" if xmode == "capi"
+                                                   else "torch.distributed all_to_all")
         if xmode == "capi":
-            cast_done[b].record(stream)
-            xstream.wait_event(cast_done[b])
+            xstream.wait_event(ce)
             exch.wire(tree, desc, wires[b], frames_out, ao=outs[b].get("ao"), stream=xstream)
             e = torch.cuda.Event()
             e.record(xstream)
             xdone[b] = e
         else:
             xdone[b] = tx.step(k, b, stream)
+        if wd:
+            recent.append((k, ce, xdone[b]))
+            wd.phase = "step %d: issued" % k
 
     def drain():
         if tx is not None:
             tx.drain(stream)
 
     step_no = 0
-    for _ in range(max(args.warmup, 2) if inflight else args.warmup):
+    if wd:
+        wd.arm(float(os.environ.get("SVO_WATCHDOG_WARMUP_S", "300")), "the warm-up steps")
+    tw = time.perf_counter()
+    n_warm = max(args.warmup, 2) if inflight else args.warmup
+    for _ in range(n_warm):
         one_step(step_no, pipe=inflight)
         step_no += 1
+    if wd:
+        wd.phase = "warm-up: draining (synchronize: waiting for the GPU)"
     drain()
     torch.cuda.synchronize()
     if world > 1:
+        wd.phase = "warm-up: barrier"
         dist.barrier()
     torch.cuda.synchronize()
+    warm_s = time.perf_counter() - tw
+    if wd:
+        wd.arm(watchdog_bound(warm_s, n_warm, args.steps), "the timed region (%d steps)" % args.steps)
     evs = [[torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)] for _ in range(args.steps)]
     reg = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     # one event pair around the timed region on the cast stream gives the average launch (gaps and the waits for the
@@ -661,12 +767,18 @@ def main():
             j.record(cstreams[1])
             stream.wait_event(j)
         reg[1].record(stream)
+    if wd:
+        wd.phase = "timed region: draining (synchronize: waiting for the GPU)"
     drain()
     torch.cuda.synchronize()
     if world > 1:
+        wd.phase = "timed region: barrier"
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if wd:
+        wd.arm(float(os.environ.get("SVO_WATCHDOG_POST_S", "300")), "the per-rank timing and the frame check after the timed region")
+        wd.phase = "after the timed region"
     kern_ms = [reg[0].elapsed_time(reg[1]) / args.steps] if region_events else [e[0].elapsed_time(e[1]) for e in evs]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -700,6 +812,12 @@ def main():
                      "how": "consecutive launches alternate between two streams (two frames in flight); each launch "
                             "itself runs longer, sharing the GPU: the per-launch roofline above is the one-at-a-time figure"}
 
+    per_rank = None
+    if world > 1:
+        per_rank = rank_timing(args, rt, torch, dist, tree, desc, outs, wires, exch, tx, xmode, gather, frames_out, cstreams[0],
+                               xstream, xdone, nbuf, step_no, nframes, W, H, dev, cdev, wd, drain, scene)
+        step_no += min(args.steps, 5)
+
     verified = None
     # N > 1: one step's displayed frames against a one-GPU cast of them, after the timed region, by default
     if (args.verify or (world > 1 and not args.no_verify)) and gather and not args.shade:
@@ -723,6 +841,8 @@ def main():
     # the job's size as the communicators report it: the C-ABI exchange's RCCL communicator
     # (svo_exchange_info), else the torch.distributed group
     n_gpus = exch.info()[1] if exch is not None else (dist.get_world_size() if world > 1 else 1)
+    if wd:
+        wd.disarm()
     if exch is not None:  # the RCCL communicator of the exchange goes before the process group's
         torch.cuda.synchronize()
         exch.close()
@@ -784,11 +904,15 @@ def main():
                    "tree_builder": builder, **({"scene_nodes": scene.info().n_nodes} if scene is not None else {})},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "build": {"libsvo_rt_sha256": rt.lib_sha256(), "library": os.path.relpath(rt.LIB_PATH, ROOT)},
+        # what carried the exchange: "rccl" (librccl.so.1 inside the C ABI), "standin" (the TEST-ONLY host-staged stand-in:
+        # never multi-GPU evidence), "torch" (torch.distributed) or null (no exchange)
+        "transport": None if not gather else ("standin" if standin else "rccl") if xmode == "capi" else "torch",
+        "build": build_block(rt),
         **({"gather_verified": verified} if (verified is not None or world > 1) else {}),
         **({"gather_verify_note": "the shaded image's exchange is not checked (gather_verified null)" if args.shade else
             "--no-verify" if args.no_verify else "no exchange (--no-gather)"} if verified is None and world > 1 else {}),
         **({"pipelined": pipelined} if pipelined is not None else {}),
+        **({"per_rank": per_rank} if per_rank is not None else {}),
         "launch_timing": "one HIP event pair around the timed region on the launch stream (average per launch, gaps "
                          "included" + ("; two frames in flight: the pair spans both cast streams" if inflight else "") + ")"
                          if region_events else "a HIP event pair around every launch on its stream (--launch-events)",
@@ -796,6 +920,99 @@ def main():
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def build_block(rt):
+    """The timed library's provenance: its file hash, the sources_sha256 stamped into it at build time (svo_build_id),
+    that stamp recomputed from the source files present here, and whether they agree (a stale library would not)"""
+    from raytracing_test_amd import build as B
+
+    stamp = rt.build_id()
+    try:
+        here = B.sources_sha256()
+    except OSError:
+        here = None
+    return {"libsvo_rt_sha256": rt.lib_sha256(), "library": os.path.relpath(rt.LIB_PATH, ROOT),
+            "sources_sha256": stamp, "sources_sha256_recomputed": here,
+            "sources_match": (stamp is not None and stamp == here) if "SVO_LIB" not in os.environ else None}
+
+
+def rank_timing(args, rt, torch, dist, tree, desc, outs, wires, exch, tx, xmode, gather, frames_out, stream, xstream, xdone, nbuf,
+                step_no, nframes, W, H, dev, cdev, wd, drain, scene):
+    """N > 1, after the timed region: every rank's own cost, so a slow rank in a scaling run can be named.  A few more
+    steps with an event pair around each cast (cast stream) and each C-ABI exchange (its stream: the RCCL send / recv
+    group plus the decode of the shards received), then the decode alone: svo_wire_scatter of this rank's own shard,
+    the display rank's cost per source shard.  Medians in ms; all ranks' figures are gathered to rank 0."""
+    nd = min(args.steps, 5)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    cast_ms, xch_ms, dec_ms = [], [], []
+    pairs = []
+    for i in range(nd):
+        k = step_no + i
+        b = k % nbuf
+        if wd:
+            wd.phase = "per-rank timing, step %d: cast" % k
+        c0, c1 = ev(), ev()
+        with torch.cuda.stream(stream):
+            if xdone[b] is not None:
+                stream.wait_event(xdone[b])
+            c0.record(stream)
+            if wires is not None:
+                tree.cast_wire(desc, wires[b], outs[b].get("ao"), stream)
+            elif args.shade:
+                tree.shade(desc, outs[b]["rgba"], out=None, stream=stream, scene=scene)
+            else:
+                tree.cast(desc, outs[b], stream)
+            c1.record(stream)
+        x0 = x1 = None
+        if gather:
+            if wd:
+                wd.phase = "per-rank timing, step %d: exchange" % k
+            if xmode == "capi":
+                x0, x1 = ev(), ev()
+                xstream.wait_event(c1)
+                x0.record(xstream)
+                exch.wire(tree, desc, wires[b], frames_out, ao=outs[b].get("ao"), stream=xstream)
+                x1.record(xstream)
+                xdone[b] = x1
+            else:
+                xdone[b] = tx.step(k, b, stream)
+        pairs.append((c0, c1, x0, x1))
+    if wd:
+        wd.phase = "per-rank timing: synchronize"
+    drain()
+    torch.cuda.synchronize()
+    for c0, c1, x0, x1 in pairs:
+        cast_ms.append(c0.elapsed_time(c1))
+        if x0 is not None:
+            xch_ms.append(x0.elapsed_time(x1))
+    if wires is not None:
+        if wd:
+            wd.phase = "per-rank timing: decode"
+        scratch = rt.Tree.alloc_hits(nframes * W * H, dev, ao=args.ao > 0)
+        for _ in range(3):
+            d0, d1 = ev(), ev()
+            d0.record(stream)
+            tree.wire_scatter(desc, wires[0], scratch, ao=outs[0].get("ao"), stream=stream)
+            d1.record(stream)
+            torch.cuda.synchronize()
+            dec_ms.append(d0.elapsed_time(d1))
+        del scratch
+    med = lambda v: float(np.median(v)) if v else float("nan")
+    mine = torch.tensor([med(cast_ms), med(xch_ms), med(dec_ms)], dtype=torch.float64, device=cdev)
+    allr = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    if wd:
+        wd.phase = "per-rank timing: all_gather"
+    dist.all_gather(allr, mine)
+    rows = []
+    for r, t in enumerate(allr):
+        c, x, d = (float(v) for v in t.cpu().numpy())
+        rows.append({"rank": r, "cast_ms": round(c, 4), "exchange_ms": None if x != x else round(x, 4),
+                     "decode_shard_ms": None if d != d else round(d, 4)})
+    return {"ranks": rows, "steps": nd,
+            "how": "after the timed region: median of %d steps with an event pair around each cast (cast stream) and each "
+                   "C-ABI exchange (its stream: RCCL send / recv group + decode of the shards received); decode_shard_ms = "
+                   "svo_wire_scatter of this rank's own shard alone (the display rank's decode cost per source shard)" % nd}
 
 
 class TorchExchange:

@@ -113,8 +113,15 @@ void initVoxelDataAllocator() {
         fprintf(stderr, "svo_bridge: initVoxelDataAllocator: device %d not available (%d visible)\n", dev, n);
         exit(1);
     }
+    if (dev != g_device) {
+        if (g_tree) g_rebuild = true;  // (a re-init onto another device re-uploads)
+        if (g_look) {  // the look-at record lives on the old device: freed there, allocated again on the new one
+            check(hipSetDevice(g_device) == hipSuccess ? 0 : SVO_EDEVICE, "hipSetDevice");
+            check(hipFree(g_look) == hipSuccess ? 0 : SVO_EDEVICE, "hipFree (look-at record)");
+            g_look = nullptr;
+        }
+    }
     check(hipSetDevice(dev) == hipSuccess ? 0 : SVO_EDEVICE, "hipSetDevice");
-    if (g_tree && dev != g_device) g_rebuild = true;  // (a re-init onto another device re-uploads)
     g_device = dev;
 }
 

@@ -60,6 +60,9 @@ typedef struct svo_tree svo_tree;   /* breadth-first linearised tree (host image
 
 const char* svo_last_error(void);
 int svo_version(void);
+/* sha256 of the sources, headers and compile flags this library was built from (raytracing_test_amd/build.py
+   sources_sha256; 64 hex digits): ties a measurement to the committed files */
+const char* svo_build_id(void);
 
 /* ---------------------------------------------------------------- world (host, editable) ---- */
 /* levels = descending tree levels; extent = 4^levels voxels per axis (reference: 5 -> 1024^3,

@@ -146,6 +146,7 @@ ABI_SYMBOLS = (
     "svo_exchange_frames", "svo_build_view", "svo_build_terrain_view", "svo_build_terrain_gpu_view",
     "svo_tree_save", "svo_tree_load", "svo_wire_bytes", "svo_cast_wire", "svo_wire_scatter", "svo_exchange_wire", "svo_tree_ceilings",
     "svo_tree_guard_trips", "svo_ceiling_layout", "svo_tree_device_ceilings", "svo_tree_device_ceiling_quads", "svo_tree_schedule", "svo_cast_ray_from_cam_async",
+    "svo_build_id",
 )
 
 
@@ -163,6 +164,15 @@ def lib_sha256():
         with open(LIB_PATH, "rb") as f:
             _lib_sha = hashlib.sha256(f.read()).hexdigest()
     return _lib_sha
+
+
+def build_id():
+    """The sources_sha256 stamped into the loaded library (svo_build_id; None for a build that predates the stamp)"""
+    L = lib()
+    if not hasattr(L, "svo_build_id"):
+        return None
+    L.svo_build_id.restype = C.c_char_p
+    return L.svo_build_id().decode()
 
 
 def ceiling_layout():

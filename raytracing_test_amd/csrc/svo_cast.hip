@@ -2533,7 +2533,7 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     // shadow rays walk t: its own column ceilings (the scene's hold for the scene's voxels, which is t's world only when
     // both trees are synced to the same edits), and t's guard-trip counter (svo_tree_guard_trips counts launches over t)
     {
-        CastParams S;
+        CastParams S{};  // (set_ceilings leaves it untouched under SVO_CAST_NO_CEILINGS: compared zeroed)
         set_ceilings(t, d, S, kCeilShade);
         const bool same = S.ceil_levels == P.ceil_levels && S.ceil_sh[0] == P.ceil_sh[0] && S.ceil_sh[1] == P.ceil_sh[1];
         P.sceilp = same ? S.ceilp : nullptr;
@@ -2556,7 +2556,11 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
         uint32_t mid = 0;
         rc = svo_tree_get_block(sc, sd->look_at[0], sd->look_at[1], sd->look_at[2], &b, &mid);
         if (rc) return rc;
-        P.look_empty = mid == 0u;  // (palette entry 0: no block)
+        // (palette entry 0: no block).  The host image runs ahead of HBM between svo_tree_update and svo_tree_sync: with
+        // edits not yet synced the device scene may still lack (or hold) that voxel, so it is taken as possibly empty
+        // there — no shading ray escapes early then, and an escaped miss cannot lose the highlight
+        const bool unsynced = sc->nodes.size() != sc->synced_nodes || !sc->dirty_nodes.empty() || sc->palette_dirty;
+        P.look_empty = mid == 0u || unsynced;
     }
     P.look_dev = reinterpret_cast<const int32_t*>(sd->look_at_dev);
     P.shadow_steps = sd->shadow_steps;

@@ -59,8 +59,15 @@ Rccl& rccl() {
     std::call_once(once, [] {
         // SVO_RCCL_LIB: another library with RCCL's entry points instead (tests/standin/rccl_standin.cpp, the test-only
         // stand-in that runs the N > 1 pairing with several ranks on one GPU), loaded locally so it shadows nothing
+        // — only with the second, explicit opt-in SVO_RCCL_STANDIN=1, so a stray SVO_RCCL_LIB cannot turn a measurement
+        // into a stand-in run; bench.py reports such runs as "transport": "standin"
         const char* over = getenv("SVO_RCCL_LIB");
-        const bool o = over && *over;
+        const char* opt = getenv("SVO_RCCL_STANDIN");
+        const bool o = over && *over && opt && strcmp(opt, "1") == 0;
+        if (over && *over && !o) {
+            R.err = "SVO_RCCL_LIB is set without SVO_RCCL_STANDIN=1 (the test-only RCCL stand-in needs both)";
+            return;
+        }
         const std::string name = o ? over : "librccl.so.1";
         void* h = dlopen(name.c_str(), o ? (RTLD_NOW | RTLD_LOCAL) : (RTLD_NOW | RTLD_GLOBAL));
         if (!h) {

@@ -145,8 +145,25 @@ bool wait_for(F pred) {
     return true;
 }
 
+// TEST HOOK (tests/test_gpu_bench_gather.py: the bench watchdog): SVO_STANDIN_WITHHOLD=<rank>:<k> drops that rank's k-th
+// send (counted over the process from 0) without a word: its receiver waits for a message that never comes, as a rank
+// stuck inside a real RCCL group would
+bool withheld(const ncclComm* c) {
+    static unsigned long long n_sends = 0;
+    const unsigned long long k = n_sends++;
+    const char* e = getenv("SVO_STANDIN_WITHHOLD");
+    int r = -1;
+    unsigned long long kk = 0;
+    return e && sscanf(e, "%d:%llu", &r, &kk) == 2 && r == c->rank && kk == k;
+}
+
 ncclResult_t do_send(const Op& op) {
     ncclComm* c = op.comm;
+    if (withheld(c)) {
+        c->send_seq[op.peer]++;
+        fprintf(stderr, "rccl_standin: rank %d: TEST HOOK withholds its send to rank %d\n", c->rank, op.peer);
+        return ncclSuccess;
+    }
     std::vector<char> host(op.bytes);
     if (c->host_only) {
         if (op.bytes) memcpy(host.data(), op.buf, op.bytes);

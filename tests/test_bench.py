@@ -161,8 +161,9 @@ def test_world_size_must_match_gpus(monkeypatch):
 
 
 def test_product_build_is_a_noop_when_up_to_date(monkeypatch, tmp_path):
-    """build() compiles nothing when libsvo_rt.so is newer than every source and header, even without its objects
-    (gpurun snapshots leave *.o behind: the GPU box must time the library the PMC passes measured)"""
+    """build() compiles nothing when libsvo_rt.so carries the stamp of the current sources, even without its objects
+    (gpurun snapshots leave *.o behind: the GPU box must time the library the PMC passes measured) and whatever the
+    files' mtimes say (tests/test_build_stamp.py: a changed source does rebuild)"""
     from raytracing_test_amd import build as b
 
     b.build()  # (up to date, or brought up to date here)
@@ -170,10 +171,50 @@ def test_product_build_is_a_noop_when_up_to_date(monkeypatch, tmp_path):
     monkeypatch.setattr(b, "_run", lambda cmd: calls.append(cmd))
     monkeypatch.setattr(b, "BUILD", str(tmp_path / "no_objects"))  # as on the box: no objects at all
     assert b.build() == b.OUT and calls == []
-    # a source newer than the library does rebuild (into the object directory it is given)
     src = os.path.join(os.path.dirname(b.__file__), "csrc", "svo_exchange.hip")
     st = os.stat(b.OUT)
     real = os.path.getmtime
     monkeypatch.setattr(os.path, "getmtime", lambda p: st.st_mtime + 10 if p == src else (real(p) if os.path.exists(p) else 0.0))
-    b.build()
-    assert any("svo_exchange.hip" in " ".join(c) for c in calls)
+    assert b.build() == b.OUT and calls == []  # newer, unchanged: no rebuild
+
+
+_WATCHDOG_CHILD = r'''
+import importlib.util, sys, time
+spec = importlib.util.spec_from_file_location("bench", sys.argv[1])
+bench = importlib.util.module_from_spec(spec)
+spec.loader.exec_module(bench)
+wd = bench.Watchdog(1, 2)
+wd.diag = lambda: "step 7: cast done, exchange PENDING"
+wd.phase = "step 7: exchange (svo_exchange_wire)"
+wd.arm(0.5, "the timed region (3 steps)")
+time.sleep(60)  # a receive that never returns
+'''
+
+
+def test_watchdog_names_the_stuck_phase_and_exits(tmp_path):
+    """The per-rank watchdog (bench.Watchdog, N > 1): past its deadline the rank reports the step, phase and GPU event
+    state, dumps every thread's traceback and exits with WATCHDOG_RC, well before the stuck call would return"""
+    import subprocess
+    import sys
+    import time
+
+    child = tmp_path / "wd.py"
+    child.write_text(_WATCHDOG_CHILD)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, str(child), os.path.join(ROOT, "bench.py")], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 124, p.stderr
+    assert time.monotonic() - t0 < 30
+    assert "rank 1 of 2: WATCHDOG: the timed region (3 steps) did not finish within 0.5 s" in p.stderr
+    assert "stuck in phase: step 7: exchange (svo_exchange_wire)" in p.stderr
+    assert "GPU events of the last steps: step 7: cast done, exchange PENDING" in p.stderr
+    assert "most recent call first" in p.stderr  # faulthandler's dump of the threads
+
+
+def test_watchdog_bound_from_the_warmup(bench, monkeypatch):
+    monkeypatch.delenv("SVO_WATCHDOG_MIN_S", raising=False)
+    monkeypatch.delenv("SVO_WATCHDOG_FACTOR", raising=False)
+    assert bench.watchdog_bound(0.5, 5, 100) == pytest.approx(204.0)  # 0.1 s per warm-up step x (100 + 2) x 20
+    assert bench.watchdog_bound(0.01, 1, 10) == 60.0  # at least a minute
+    monkeypatch.setenv("SVO_WATCHDOG_MIN_S", "10")
+    monkeypatch.setenv("SVO_WATCHDOG_FACTOR", "1")
+    assert bench.watchdog_bound(2.0, 1, 3) == 10.0

@@ -94,7 +94,7 @@ def test_capi_exchange_on_one_gpu(n, extra, tmp_path):
         pytest.skip("no GPU")
     assert os.path.exists(STANDIN), "the stand-in is not built (raytracing_test_amd/build.py build_rccl_standin)"
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
-    env.update(SVO_RCCL_LIB=STANDIN, SVO_STANDIN_DIR=str(tmp_path), SVO_STANDIN_TIMEOUT_S="60")
+    env.update(SVO_RCCL_LIB=STANDIN, SVO_RCCL_STANDIN="1", SVO_STANDIN_DIR=str(tmp_path), SVO_STANDIN_TIMEOUT_S="60")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--dist-backend", "gloo", "--exchange", "capi",
            "--steps", "3", "--warmup", "1", "--no-cpu-baseline"] + list(extra)
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
@@ -105,5 +105,37 @@ def test_capi_exchange_on_one_gpu(n, extra, tmp_path):
     assert d["n_gpus"] == n  # svo_exchange_info of the communicator the step ran over
     assert d["config"]["exchange"].startswith("svo_cast_wire + svo_exchange_wire") and "stand-in" in d["config"]["exchange"], d
     assert d["scaling"] == ("strong" if "--frames" in extra else "weak")
+    assert d["transport"] == "standin", d  # (never to be read as RCCL multi-GPU evidence)
+    ranks = d["per_rank"]["ranks"]  # every rank's own cast / exchange / decode cost (a slow rank can be named)
+    assert [r["rank"] for r in ranks] == list(range(n))
+    assert all(r["cast_ms"] > 0 and r["exchange_ms"] is not None and r["exchange_ms"] > 0 and r["decode_shard_ms"] > 0 for r in ranks), ranks
     assert d["gather_verified"] is True, d
     assert [x for x in os.listdir(tmp_path) if x.startswith("svo_rccl_standin_")] == []  # every message was received
+
+
+def test_stalled_receive_ends_the_run(tmp_path):
+    """A receive that never completes (the stand-in's test hook withholds rank 1's third send, a timed step's) must not
+    hang the job: the stuck ranks' watchdogs fire within their bound (here at least 10 s: SVO_WATCHDOG_MIN_S, factor 1
+    over the warm-up's time per step), name the step and phase on stderr, and the run exits with WATCHDOG_RC (124)
+    instead of waiting for the stand-in's own 600-s receive timeout"""
+    import time
+
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert os.path.exists(STANDIN), "the stand-in is not built (raytracing_test_amd/build.py build_rccl_standin)"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(SVO_RCCL_LIB=STANDIN, SVO_RCCL_STANDIN="1", SVO_STANDIN_DIR=str(tmp_path), SVO_STANDIN_TIMEOUT_S="600",
+               SVO_STANDIN_WITHHOLD="1:2", SVO_WATCHDOG_MIN_S="10", SVO_WATCHDOG_FACTOR="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--exchange", "capi",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    t0 = time.monotonic()
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=200, cwd=ROOT, env=env)
+    took = time.monotonic() - t0
+    assert p.returncode == 124, (p.returncode, p.stderr[-3000:])
+    assert "TEST HOOK withholds" in p.stderr
+    assert "rank 0 of 2: WATCHDOG: the timed region" in p.stderr, p.stderr[-3000:]
+    assert "stuck in phase: step 2: exchange" in p.stderr, p.stderr[-3000:]  # rank 0 waits for rank 1's step-2 message
+    assert "GPU events of the last steps" in p.stderr
+    assert took < 150, took

@@ -89,6 +89,24 @@ def test_collapse_builder_equals_putblock(oracle_mod):
     assert np.array_equal(fa, fb) and np.array_equal(ca, cb)
 
 
+@pytest.mark.parametrize("levels", [6, 7])
+def test_collapse_builder_equals_putblock_at_config_depths(oracle_mod, levels):
+    """The collapse builder behind the C3 (6 levels) and C5 (7 levels) oracle trees against the reference's own
+    construction, genWorld's putBlock per voxel (tetrahexa_tree.cpp:176-291, world_gen.cpp:13-42), at those depths: a
+    512 x 512-column patch at the world origin, every voxel of its bounding box (and a margin of empty columns past
+    it) compared — flags and colour"""
+    n = 512
+    A = oracle_mod.Tree.terrain(levels, n, n)
+    B = oracle_mod.Tree.terrain_putblock(levels, n, n)
+    ra, fa, ca = A.dump_box(0, 0, 0, n + 8, 72, n + 8)
+    rb, fb, cb = B.dump_box(0, 0, 0, n + 8, 72, n + 8)
+    assert ra == 0 and rb == 0
+    assert np.array_equal(fa, fb) and np.array_equal(ca, cb)
+    assert (fa[:, :, :n] != 0).any() and (fa[:, :, n:] == 0).all() and (fa[n:] == 0).all()  # solid inside, empty past it
+    h = oracle_mod.heights(n, n)
+    assert int(h.max()) < 72  # the box holds every column's top
+
+
 def test_terrain_height_range(oracle_mod):
     r = facts()["terrain_4096_height_range"]
     h = oracle_mod.heights(4096, 4096)

@@ -12,7 +12,7 @@ d() { local name=$1 n=$2 port=$3; shift 3; echo "[evidence] $(date +%T) $name"; 
 # the C-ABI exchange at N > 1 (svo_cast_wire + svo_exchange_wire, ncclGroupStart/Send/Recv/GroupEnd) with N ranks on
 # this one GPU: libsvo_rt dlopens the TEST-ONLY host-staged stand-in (SVO_RCCL_LIB) in place of RCCL, which cannot form a
 # communicator of N ranks on one device; bench.py verifies the displayed frames at N > 1 by default
-s() { local name=$1 n=$2; shift 2; echo "[evidence] $(date +%T) $name"; mkdir -p $OUT/standin_$name; SVO_RCCL_LIB=$PWD/tests/standin/_build/librccl_standin.so SVO_STANDIN_DIR=$OUT/standin_$name SVO_STANDIN_TIMEOUT_S=60 timeout -k 10 300 python bench.py --gpus $n --dist-backend gloo --exchange capi --no-cpu-baseline "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$name.err; exit $rc; }; grep '^{' $OUT/bench_$name.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['n_gpus'], d['scaling'], round(d['value']/1e6,1), 'M rays/s', 'verified', d.get('gather_verified'))"; }
+s() { local name=$1 n=$2; shift 2; echo "[evidence] $(date +%T) $name"; mkdir -p $OUT/standin_$name; SVO_RCCL_LIB=$PWD/tests/standin/_build/librccl_standin.so SVO_RCCL_STANDIN=1 SVO_STANDIN_DIR=$OUT/standin_$name SVO_STANDIN_TIMEOUT_S=60 timeout -k 10 300 python bench.py --gpus $n --dist-backend gloo --exchange capi --no-cpu-baseline "$@" > $OUT/bench_$name.json 2> $OUT/bench_$name.err; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_$name.err; exit $rc; }; grep '^{' $OUT/bench_$name.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['n_gpus'], d['scaling'], round(d['value']/1e6,1), 'M rays/s', 'verified', d.get('gather_verified'))"; }
 b c3
 b c3f --config c3f
 b c1 --config c1
