@@ -34,3 +34,9 @@ void svoRenderShaded(int32_t width, int32_t height, float* rgba, hipStream_t str
 svo_tree* svoTree();
 // the full-view scene tree svoRenderShaded's rays walk
 svo_tree* svoScene();
+// svoRenderShaded's image on screen (bridge/svo_present_gl.cpp, needs the application's GL context): rendered into a
+// HIP-registered GL pixel buffer, uploaded to a texture and blitted to the default framebuffer — the replacement of
+// render()'s glUseProgram(lowResProgram) / glDrawArrays (src/main.cpp:73,105-107)
+void svoPresentShaded(int32_t width, int32_t height, float time = 0.0f, hipStream_t stream = nullptr);
+// frees its GL objects and the HIP registration (before the GL context goes)
+void svoPresentRelease();

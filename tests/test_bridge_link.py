@@ -63,3 +63,29 @@ def test_main_shape_links_without_voxel_allocator(built):
     for s in SYMS:
         assert syms.get(s) == "T", (s, syms.get(s))
     assert not any(k.endswith(("arrayBlocks", "nodeBlocks")) for k in syms)
+
+
+def test_gl_present_helper_compiles_and_links(built, tmp_path):
+    """bridge/svo_present_gl.cpp (svoPresentShaded: svoRenderShaded into a HIP-registered GL pixel buffer, a texture
+    upload and a blit — what replaces render()'s glDrawArrays, main.cpp:105-107) compiles against the system GL
+    headers and hip_gl_interop.h, and a main.cpp-shaped program links with it, the shim and libsvo_rt, every GL entry
+    point from libGL and every HIP one from libamdhip64 (no GL context here: nothing is run)"""
+    gl = [d for d in ("/usr/lib/x86_64-linux-gnu", "/usr/lib64", "/usr/lib") if os.path.exists(os.path.join(d, "libGL.so"))]
+    if not os.path.exists("/usr/include/GL/glext.h") or not gl:
+        pytest.skip("no GL headers / libGL in this image")
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    obj = str(tmp_path / "svo_present_gl.o")
+    inc = ["-I" + os.path.join(rocm, "include"), "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "tests", "bridge"),
+           "-I" + os.path.join(ROOT, "bridge"), "-I" + os.path.join(ROOT, "bridge", "reference")]
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__"] + inc +
+                   ["-c", os.path.join(ROOT, "bridge", "svo_present_gl.cpp"), "-o", obj], check=True)
+    syms = _nm(obj)
+    assert syms.get("_Z16svoPresentShadediifP12ihipStream_t") == "T"
+    for s in ("hipGraphicsGLRegisterBuffer", "hipGraphicsMapResources", "hipGraphicsResourceGetMappedPointer",
+              "hipGraphicsUnmapResources", "glTexSubImage2D", "glBlitFramebuffer", "_Z15svoRenderShadediiPfP12ihipStream_tf"):
+        assert syms.get(s) == "U", s
+    prog = str(tmp_path / "main_shape_gl")
+    from raytracing_test_amd import build as b
+    subprocess.run(["g++", os.path.join(built, "main_shape.o"), os.path.join(built, "svo_bridge.o"), obj, "-L" + b.HERE, "-lsvo_rt",
+                    "-L" + os.path.join(rocm, "lib"), "-lamdhip64", "-L" + gl[0], "-lGL", "-o", prog], check=True)
+    assert _nm(prog).get("_Z16svoPresentShadediifP12ihipStream_t") == "T"
