@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 #include <type_traits>
 #include <string>
 #include <utility>
@@ -80,6 +81,7 @@ struct CastParams {
     const uint32_t* mat_flags;
     float4* rgba;
     float sun[3];
+    int32_t sun_dirs;  // the shadow rays' step-sign octant (dirs_sign numbering, 1..8): every shadow ray steps with the sun's signs
     int32_t look[3];
     int32_t look_valid, shadow_steps;
     int32_t look_empty;         // the host look-at voxel is not stored in the scene (an escaped ray could end on it)
@@ -120,7 +122,9 @@ constexpr int kSchedGroup = SVO_SCHED_GROUP;  // frame schedules order groups of
 // trace on the camera's octant (profiles/r05/shade_split_ab.json); 8 with the bounce state in registers spilled 22 VGPRs.
 // The generic-sign instance (no octant) runs 6 (80 VGPRs: 7 would spill 29)
 constexpr int kShadeWaves = 7;
-constexpr int kMaxLevels = 7;  // svo_world_create / svo_build_terrain bound
+#ifndef SVO_X_PRIMARY_WAVES
+#define SVO_X_PRIMARY_WAVES 8
+#endif
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -798,7 +802,7 @@ __device__ __forceinline__ bool ceil_march(const CastParams& P, const uint32_t* 
         // the next boundary lies beyond the budget: only the ceiling event can come first within it
         const bool far = (xn ? jx : jz) > R.steps;
         if (!(Eexit < tc) || Ex == Ez || far) {
-            if (far || !(Ez <= tc && Ez <= Ex) && tc <= Ex) {  // the first unproven event, in the DDA's order at ties: z, y, x
+            if (far || (!(Ez <= tc && Ez <= Ex) && tc <= Ex)) {  // the first unproven event, in the DDA's order at ties: z, y, x
                 stop_axis = 1;
                 stop_j = jy;
             } else if (Ez <= tc && Ez <= Ex) {
@@ -1079,6 +1083,22 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // move instead of one per 256-column block; its budget ends in it or it wraps in y)
             if (ESCAPE) gt = top >= 0 && y > top;
         }
+#if SVO_X_INLOOP_MARCH == 2
+        if (MARCH && ceil_on && __ballot(!(cl && !gt && (SEG ? lin : fast) && R.s[1] < 0 && R.steps > 0)) == 0ull) {
+            int32_t mex[3];
+            if (ceil_march<STATS>(P, ceilp, R, wm, mex, st)) {
+                if (skip_box<TRACK, RB>(R, mex, wseg)) {
+                    uint32_t wn[3];
+                    wrap3(R, wm, wn);
+                    jump = moved | (w[0] ^ wn[0]) | (w[1] ^ wn[1]) | (w[2] ^ wn[2]);
+                } else {
+                    done = true;
+                    if (ESCAPE && top >= 0) escaped = true;
+                }
+                continue;
+            }
+        }
+#endif
         // (the box exits are taken only when a lane of the wave moves — wave-uniform; with the forward boxes gated
         // the same way, 1.1 % faster at C3 than per-lane selects: profiles/r03/ab_r03_x_*.log)
         any_cl = ceil_on && __ballot(cl) != 0ull;
@@ -1097,6 +1117,15 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             cex[0] = gt ? R.steps : (int32_t)(R.s[0] > 0 ? bmk - (w[0] & bmk) : (w[0] & bmk));
             cex[1] = R.s[1] < 0 ? y - (gt ? top : c) - 1 : (int32_t)(wm - w[1]);
             cex[2] = gt ? R.steps : (int32_t)(R.s[2] > 0 ? bmk - (w[2] & bmk) : (w[2] & bmk));
+#if SVO_X_INLOOP_MARCH
+            if (MARCH && cl && !gt && (SEG ? lin : fast) && R.s[1] < 0) {
+                int32_t mex[3];
+                if (ceil_march<STATS>(P, ceilp, R, wm, mex, st)) {
+#pragma unroll
+                    for (int k = 0; k < 3; k++) cex[k] = mex[k];
+                }
+            }
+#endif
         }
         uint32_t kind = R_CEIL;
         if (!cl) {
@@ -1561,6 +1590,12 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
                                      (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
                 // (DIRS: a sign octant every shadow ray of the launch steps with; shading launches pass 0 — their instances are
                 // specialised on the camera's octant instead, k_cast)
+#if SVO_X_SUN_OCTANT
+                if (DIRS == 0 && P.sun_dirs == 1)  // (uniform) the reference's sun, normalize(2, 1, 4) (globals.cpp:23): every step +
+                    dark = (trace<false, false, true, false, 1, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr,
+                                                                          P.top_solid).info & HIT_BIT) != 0u;
+                else
+#endif
                 dark = (trace<false, false, true, false, DIRS, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                             .info & HIT_BIT) != 0u;
             }
@@ -1623,7 +1658,7 @@ template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int
 // the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
 // against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 7 waves on the camera's
 // octant (kShadeWaves), 6 with generic signs
-__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWaves : 6) : 8)) void k_cast(const CastParams P) {
+__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWaves : 6) : SVO_X_PRIMARY_WAVES)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1922,41 +1957,35 @@ bool wide_nodes(const svo_tree* t, int32_t flags) { return t->dev_node_cap >= kN
 // The per-lane LDS path of k_cast (Path): 3 dwords per interior depth (levels - 1 of them) per lane of the block
 size_t path_lds(const CastParams& P) { return (size_t)(P.levels > 1 ? P.levels - 1 : 1) * 3 * kBlock * sizeof(uint32_t); }
 
-// seg: an instance with segment-bounded crossings (rays from non-integral origins; shading always);
-// dirs: frame_dirs (the plain primary instance of narrow trees has one per sign octant)
-template <bool AO, bool SEG>
-void launch_dirs(int dirs, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
-    switch (dirs) {
-        case 1: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 1>), grid, block, path_lds(P), st, P); return;
-        case 2: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 2>), grid, block, path_lds(P), st, P); return;
-        case 3: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 3>), grid, block, path_lds(P), st, P); return;
-        case 4: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 4>), grid, block, path_lds(P), st, P); return;
-        case 5: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 5>), grid, block, path_lds(P), st, P); return;
-        case 6: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 6>), grid, block, path_lds(P), st, P); return;
-        case 7: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 7>), grid, block, path_lds(P), st, P); return;
-        default: hipLaunchKernelGGL((k_cast<false, false, AO, false, false, SEG, 8>), grid, block, path_lds(P), st, P); return;
-    }
+// The sign-octant instances (dirs 1..8, frame_dirs) of one family, as a table built at compile time: launch block b of the
+// primary casts (AO or not, SEG or not) and of the shading pass's straight trace (with / without hit records) picks its
+// kernel by index instead of a hand-written case per octant
+using CastKernel = void (*)(CastParams);
+template <bool AO, bool SHADE, bool SEG, bool NOREC, size_t... I>
+constexpr std::array<CastKernel, sizeof...(I)> octant_kernels(std::index_sequence<I...>) {
+    return {{&k_cast<false, false, AO, SHADE, false, SEG, (int)I + 1, NOREC>...}};
+}
+template <bool AO, bool SHADE, bool SEG, bool NOREC = false>
+void launch_octant(int dirs, dim3 grid, dim3 block, hipStream_t st, const CastParams& P) {
+    static constexpr std::array<CastKernel, 8> tab = octant_kernels<AO, SHADE, SEG, NOREC>(std::make_index_sequence<8>());
+    CastParams arg = P;
+    void* args[] = {&arg};
+    (void)hipLaunchKernel(reinterpret_cast<const void*>(tab[(dirs >= 1 && dirs <= 8 ? dirs : 8) - 1]), grid, block, args, path_lds(P), st);
 }
 template <bool STATS, bool STAMPS, bool AO, bool SHADE>
 void launch_cast(bool wide, bool seg, dim3 grid, dim3 block, hipStream_t st, const CastParams& P, int dirs = 0) {
     if (!STATS && !STAMPS && !SHADE && !wide && dirs) {  // (narrow trees: below 2^28 nodes)
-        if (seg) launch_dirs<AO, true>(dirs, grid, block, st, P);
-        else launch_dirs<AO, false>(dirs, grid, block, st, P);
+        if (seg) launch_octant<AO, false, true>(dirs, grid, block, st, P);
+        else launch_octant<AO, false, false>(dirs, grid, block, st, P);
         return;
     }
     // the camera's octant (the straight trace of the shading rays); without hit records, a launch whose every origin is
     // exact (seg: need_seg false) takes the straight trace without segment bounds (the bouncing trace keeps them)
     if (SHADE && !STATS && !wide && dirs) {
-        switch (dirs) {
-            case 1: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 1, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 1, true>), grid, block, path_lds(P), st, P); return;
-            case 2: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 2, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 2, true>), grid, block, path_lds(P), st, P); return;
-            case 3: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 3, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 3, true>), grid, block, path_lds(P), st, P); return;
-            case 4: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 4, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 4, true>), grid, block, path_lds(P), st, P); return;
-            case 5: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 5, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 5, true>), grid, block, path_lds(P), st, P); return;
-            case 6: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 6, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 6, true>), grid, block, path_lds(P), st, P); return;
-            case 7: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 7, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 7, true>), grid, block, path_lds(P), st, P); return;
-            default: if (P.pos) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8>), grid, block, path_lds(P), st, P); else if (seg) hipLaunchKernelGGL((k_cast<false, false, false, true, false, true, 8, true>), grid, block, path_lds(P), st, P); else hipLaunchKernelGGL((k_cast<false, false, false, true, false, false, 8, true>), grid, block, path_lds(P), st, P); return;
-        }
+        if (P.pos) launch_octant<false, true, true>(dirs, grid, block, st, P);
+        else if (seg) launch_octant<false, true, true, true>(dirs, grid, block, st, P);
+        else launch_octant<false, true, false, true>(dirs, grid, block, st, P);
+        return;
     }
     if (SHADE || seg) {
         if (wide) hipLaunchKernelGGL((k_cast<STATS, STAMPS, AO, SHADE, true, true>), grid, block, path_lds(P), st, P);
@@ -2546,8 +2575,10 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     P.top_scene = sc->dev_top_y;
     P.top_solid = t->dev_top_y;
     P.rgba = reinterpret_cast<float4*>(rgba);
+    P.sun_dirs = 1;
     for (int k = 0; k < 3; k++) {
         P.sun[k] = sd->sun_dir[k];
+        P.sun_dirs += (sd->sun_dir[k] < 0.0f ? 1 : 0) << k;  // (dda_axis' step: -1 only below zero; -0.0 and NaN step +)
         P.look[k] = sd->look_at[k];
     }
     P.look_valid = sd->look_at_valid != 0;
