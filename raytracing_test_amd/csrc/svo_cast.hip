@@ -122,9 +122,6 @@ constexpr int kSchedGroup = SVO_SCHED_GROUP;  // frame schedules order groups of
 // trace on the camera's octant (profiles/r05/shade_split_ab.json); 8 with the bounce state in registers spilled 22 VGPRs.
 // The generic-sign instance (no octant) runs 6 (80 VGPRs: 7 would spill 29)
 constexpr int kShadeWaves = 7;
-#ifndef SVO_X_PRIMARY_WAVES
-#define SVO_X_PRIMARY_WAVES 8
-#endif
 
 struct Hit {
     int32_t x, y, z, steps_left;
@@ -1001,8 +998,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         }
     }
     // one back-edge: every path through the body ends at the loop latch
-    uint32_t bref = 0u, binfo = 0u;
-    uint64_t bmask = 0ull;
     bool escaped = false;
     // coordinate bits changed since the last voxel known to lie in the parent's region, by ceiling moves since
     // the last lookup and the step before them (the lookup's restart depth)
@@ -1038,6 +1033,10 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         }
         uint32_t sh = 0u;
         bool pend = false;  // the lookup found a brick: step through it below
+        // the region the lookup finds (read only for BRICK / SOLID results, which the lookup writes in this iteration):
+        // per iteration, so nothing of the last iteration's brick is carried around the loop in registers
+        uint32_t bref = 0u, binfo = 0u;
+        uint64_t bmask = 0ull;
         const uint32_t ax = R.axis;
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
@@ -1083,22 +1082,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             // move instead of one per 256-column block; its budget ends in it or it wraps in y)
             if (ESCAPE) gt = top >= 0 && y > top;
         }
-#if SVO_X_INLOOP_MARCH == 2
-        if (MARCH && ceil_on && __ballot(!(cl && !gt && (SEG ? lin : fast) && R.s[1] < 0 && R.steps > 0)) == 0ull) {
-            int32_t mex[3];
-            if (ceil_march<STATS>(P, ceilp, R, wm, mex, st)) {
-                if (skip_box<TRACK, RB>(R, mex, wseg)) {
-                    uint32_t wn[3];
-                    wrap3(R, wm, wn);
-                    jump = moved | (w[0] ^ wn[0]) | (w[1] ^ wn[1]) | (w[2] ^ wn[2]);
-                } else {
-                    done = true;
-                    if (ESCAPE && top >= 0) escaped = true;
-                }
-                continue;
-            }
-        }
-#endif
         // (the box exits are taken only when a lane of the wave moves — wave-uniform; with the forward boxes gated
         // the same way, 1.1 % faster at C3 than per-lane selects: profiles/r03/ab_r03_x_*.log)
         any_cl = ceil_on && __ballot(cl) != 0ull;
@@ -1117,15 +1100,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
             cex[0] = gt ? R.steps : (int32_t)(R.s[0] > 0 ? bmk - (w[0] & bmk) : (w[0] & bmk));
             cex[1] = R.s[1] < 0 ? y - (gt ? top : c) - 1 : (int32_t)(wm - w[1]);
             cex[2] = gt ? R.steps : (int32_t)(R.s[2] > 0 ? bmk - (w[2] & bmk) : (w[2] & bmk));
-#if SVO_X_INLOOP_MARCH
-            if (MARCH && cl && !gt && (SEG ? lin : fast) && R.s[1] < 0) {
-                int32_t mex[3];
-                if (ceil_march<STATS>(P, ceilp, R, wm, mex, st)) {
-#pragma unroll
-                    for (int k = 0; k < 3; k++) cex[k] = mex[k];
-                }
-            }
-#endif
         }
         uint32_t kind = R_CEIL;
         if (!cl) {
@@ -1590,12 +1564,13 @@ __device__ __forceinline__ void shade_out(const CastParams& P, const Mem& smem, 
                                      (float)(h.z - (ax == 2u ? sg : 0)) + 0.5f};
                 // (DIRS: a sign octant every shadow ray of the launch steps with; shading launches pass 0 — their instances are
                 // specialised on the camera's octant instead, k_cast)
-#if SVO_X_SUN_OCTANT
-                if (DIRS == 0 && P.sun_dirs == 1)  // (uniform) the reference's sun, normalize(2, 1, 4) (globals.cpp:23): every step +
+                // the reference's sun, normalize(2, 1, 4) (globals.cpp:23; uniform), steps + on every axis: its octant is
+                // compiled into a second copy of the shadow trace (shaded C3 -3.0 %, profiles/r06/ab_sun_octant_shadows.txt);
+                // any other sun takes per-wave sign flags
+                if (DIRS == 0 && P.sun_dirs == 1)
                     dark = (trace<false, false, true, false, 1, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr,
                                                                           P.top_solid).info & HIT_BIT) != 0u;
                 else
-#endif
                 dark = (trace<false, false, true, false, DIRS, false, 3>(P, smem, P.smats, path, so, P.sun, P.shadow_steps, nullptr, nullptr, nullptr, P.top_solid)
                             .info & HIT_BIT) != 0u;
             }
@@ -1658,7 +1633,7 @@ template <bool STATS, bool STAMPS, bool AO, bool SHADE, bool WIDE, bool SEG, int
 // the hemisphere table read from the kernel arguments instead of LDS, the LDS allows 8 waves: C4 0.2441 -> 0.2311 ms
 // against 6 waves at 79 VGPRs, 0.2349 at 7); the diagnostics instances 6; the shading instances 7 waves on the camera's
 // octant (kShadeWaves), 6 with generic signs
-__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWaves : 6) : SVO_X_PRIMARY_WAVES)) void k_cast(const CastParams P) {
+__global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWaves : 6) : 8)) void k_cast(const CastParams P) {
     using Mem = typename std::conditional<WIDE, WideNodes, BufNodes>::type;
     const Mem mem(P.nodes);
     const Mem smem(SHADE ? P.snodes : P.nodes);  // shading: shadow rays walk the solid view
@@ -1741,7 +1716,13 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWav
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO, 1>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
         if (!SHADE && P.wire) {  // (wave-uniform: one launch writes one kind of record)
-            wire_put(P.wire, P.wire_compact != 0, out, o, h.x, h.y, h.z, h.t, h.info);
+            // the origin read again (frame mode: the frame's, uniform; explicit: the ray's) rather than kept in three VGPRs
+            // through the whole trace
+            float oo[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                oo[k] = P.mode == MODE_FRAME ? P.frame_org[3 * frm + k] : (P.mode == MODE_EXPLICIT && P.rorg ? P.rorg[3 * g + k] : P.org[k]);
+            wire_put(P.wire, P.wire_compact != 0, out, oo, h.x, h.y, h.z, h.t, h.info);
         } else {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
