@@ -999,6 +999,8 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     }
     // one back-edge: every path through the body ends at the loop latch
     bool escaped = false;
+    uint32_t bref = 0u, binfo = 0u;
+    uint64_t bmask = 0ull;
     // coordinate bits changed since the last voxel known to lie in the parent's region, by ceiling moves since
     // the last lookup and the step before them (the lookup's restart depth)
     uint32_t jump = 0u;
@@ -1033,10 +1035,6 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
         }
         uint32_t sh = 0u;
         bool pend = false;  // the lookup found a brick: step through it below
-        // the region the lookup finds (read only for BRICK / SOLID results, which the lookup writes in this iteration):
-        // per iteration, so nothing of the last iteration's brick is carried around the loop in registers
-        uint32_t bref = 0u, binfo = 0u;
-        uint64_t bmask = 0ull;
         const uint32_t ax = R.axis;
         const uint32_t wa = ax == 0u ? w[0] : (ax == 1u ? w[1] : w[2]);
         const int32_t sa = ax == 0u ? R.s[0] : (ax == 1u ? R.s[1] : R.s[2]);
@@ -1716,13 +1714,7 @@ __global__ __launch_bounds__(kBlock, STATS ? 6 : (SHADE ? (DIRS != 0 ? kShadeWav
         const Hit h = trace<STATS, false, false, SEG, DIRS, AO, 1>(P, mem, P.mats, path, o, d, P.steps, P.stats ? P.stats + SVO_STATS_HEADER + 2 * (int64_t)gridDim.x * (kBlock / 64) + out : nullptr,
                                    nullptr, AO ? &pfin : nullptr, -1, P.top_solid, DIRS != 0 ? &P.fax[frm] : nullptr);
         if (!SHADE && P.wire) {  // (wave-uniform: one launch writes one kind of record)
-            // the origin read again (frame mode: the frame's, uniform; explicit: the ray's) rather than kept in three VGPRs
-            // through the whole trace
-            float oo[3];
-#pragma unroll
-            for (int k = 0; k < 3; k++)
-                oo[k] = P.mode == MODE_FRAME ? P.frame_org[3 * frm + k] : (P.mode == MODE_EXPLICIT && P.rorg ? P.rorg[3 * g + k] : P.org[k]);
-            wire_put(P.wire, P.wire_compact != 0, out, oo, h.x, h.y, h.z, h.t, h.info);
+            wire_put(P.wire, P.wire_compact != 0, out, o, h.x, h.y, h.z, h.t, h.info);
         } else {
             reinterpret_cast<int4*>(P.pos)[out] = make_int4(h.x, h.y, h.z, h.steps_left);
             P.t[out] = h.t;
