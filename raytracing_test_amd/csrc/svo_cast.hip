@@ -2548,10 +2548,10 @@ extern "C" int svo_shade_rays(const svo_tree* t, const svo_cast_desc* d, const s
     P.top_scene = sc->dev_top_y;
     P.top_solid = t->dev_top_y;
     P.rgba = reinterpret_cast<float4*>(rgba);
-    P.sun_dirs = 1;
+    P.sun_dirs = (d->flags & SVO_CAST_NO_OCTANT) ? 0 : 1;  // (0: per-wave sign flags for the shadow rays as well)
     for (int k = 0; k < 3; k++) {
         P.sun[k] = sd->sun_dir[k];
-        P.sun_dirs += (sd->sun_dir[k] < 0.0f ? 1 : 0) << k;  // (dda_axis' step: -1 only below zero; -0.0 and NaN step +)
+        if (P.sun_dirs) P.sun_dirs += (sd->sun_dir[k] < 0.0f ? 1 : 0) << k;  // (dda_axis' step: -1 only below zero; -0.0, NaN: +)
         P.look[k] = sd->look_at[k];
     }
     P.look_valid = sd->look_at_valid != 0;

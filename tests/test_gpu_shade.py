@@ -296,6 +296,21 @@ def test_shade_escape_is_exact(rt, gtree, lake_scene, cam):
         assert np.array_equal(f2.cpu().numpy(), g2.cpu().numpy()), (cam, S)
 
 
+@pytest.mark.parametrize("sun", [None, (2.0, -1.0, 4.0), (-2.0, 1.0, -4.0)])
+def test_shadow_octant_equals_sign_flags(rt, gtree, lake_scene, sun):
+    """Shadow rays of the reference sun, normalize(2, 1, 4) (globals.cpp:23), run a copy of the trace with that step
+    octant compiled in; SVO_CAST_NO_OCTANT gives every shadow (and primary) ray per-wave sign flags instead.  The images
+    are identical, for that sun and for suns of other octants (which take the flags either way)."""
+    org, cd = LAKE_CAMERAS[1]  # looking down into a lake: lit and shadowed faces
+    cam_dir = rt.normalize(cd)
+    s = rt.sun_dir() if sun is None else tuple(rt.normalize(sun))
+    a = gtree.shade_frame(org, cam_dir, 200, 120, 5000, sun=s, scene=lake_scene, time=0.5)
+    b = gtree.shade_frame(org, cam_dir, 200, 120, 5000, sun=s, scene=lake_scene, time=0.5, flags=rt.CAST_NO_OCTANT)
+    assert np.array_equal(a.cpu().numpy(), b.cpu().numpy())
+    c = gtree.shade_frame(org, cam_dir, 200, 120, 5000, sun=s, scene=lake_scene, time=0.5, shadow_steps=0)
+    assert not np.array_equal(a.cpu().numpy(), c.cpu().numpy())  # (the shadow rays darken some pixels: exercised)
+
+
 def test_shade_bench_scene_full_frame(rt, depth12, oracle12, torch_cuda):
     """The shaded workload bench.py --shade times, every pixel: the GPU-built 4096^2-column solid and full-view
     (water) trees, the C3 pose, S = 16384, the reference sun; the image without hit records (the bench's form:
