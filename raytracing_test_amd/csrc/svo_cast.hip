@@ -555,8 +555,10 @@ constexpr uint64_t kNarrowNodes = 1ull << 28;  // below it, ni1 << 4 stays below
 
 struct BufNodes {
     __amdgpu_buffer_rsrc_t rsrc;
+    const Node* __restrict__ base;
     __device__ __forceinline__ explicit BufNodes(const Node* p)
-        : rsrc(__builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(p - 1), (short)0, (int)0xFFFFFFFFu, (int)0x00020000)) {}
+        : rsrc(__builtin_amdgcn_make_buffer_rsrc(const_cast<Node*>(p - 1), (short)0, (int)0xFFFFFFFFu, (int)0x00020000)), base(p) {}
+    __device__ __forceinline__ Node root() const { return base[0]; }  // (uniform: a scalar load)
     __device__ __forceinline__ Node load(uint32_t ni) const {  // node ni - 1
         const uint32_t off = ni << 4;
         Node n;
@@ -571,7 +573,9 @@ struct BufNodes {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct WideNodes {
     const __attribute__((address_space(1))) u32x4* p;
-    __device__ __forceinline__ explicit WideNodes(const Node* q) : p((const __attribute__((address_space(1))) u32x4*)(q - 1)) {}
+    const Node* __restrict__ base;
+    __device__ __forceinline__ explicit WideNodes(const Node* q) : p((const __attribute__((address_space(1))) u32x4*)(q - 1)), base(q) {}
+    __device__ __forceinline__ Node root() const { return base[0]; }  // (uniform: a scalar load)
     __device__ __forceinline__ Node load(uint32_t ni) const {  // node ni - 1
         const u32x4 v = p[ni];  // 64-bit address: base + (u64)ni * 16
         Node n;
@@ -966,11 +970,24 @@ __device__ __forceinline__ Hit trace(const CastParams& P, const Mem& mem, const 
     const uint32_t wm = P.wmask;
     Stats st = {0, 0, 0, 0, 0, 0, {0, 0, 0, 0}, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     Parent par;
-    // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
-    // the whole world = node 0): the first lookup takes the same path as every later one
-    par.mask = 1ull;
-    par.ref = 0u;
-    par.sh = 2u * (uint32_t)P.levels;
+    // the root (node 0 of the tree this trace walks; uniform, one scalar load) is the first parent and stands in the
+    // per-lane path at depth 0, so the first lookup starts at the root's child slot instead of loading the root (one
+    // dependent load fewer per ray; every later restart at depth 0 reads the same node from the path: C3 -0.8 %, C4
+    // -0.6 %, C5 -1.1 %, shaded -0.5 %, profiles/r06/ab_root_seed_*.txt).  A root that is not interior (a one-level
+    // tree, a uniform world) keeps the virtual parent above it.
+    const Node rn = mem.root();
+    if (P.levels >= 2 && (rn.info & K_KIND_MASK) == K_INTERIOR) {  // (uniform)
+        path.put(0, rn.mask, rn.ref);
+        par.mask = rn.mask;
+        par.ref = rn.ref;
+        par.sh = 2u * (uint32_t)(P.levels - 1);
+    } else {
+        // a virtual parent above the root (its one child region, slot 0 of the wrapped coordinates, is
+        // the whole world = node 0): the first lookup takes the same path as every later one
+        par.mask = 1ull;
+        par.ref = 0u;
+        par.sh = 2u * (uint32_t)P.levels;
+    }
     // XS 2: resume a ray from the state its straight trace (XS 1) stopped in — the cell it entered, untested; the
     // flags above (fast, lin: from the origin and direction) are the ones that trace had
     bool done = R.steps <= 0;
