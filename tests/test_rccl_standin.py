@@ -129,3 +129,39 @@ def test_standin_rank_joining_after_the_others_left(standin, tmp_path):
     outs = _ranks(standin, tmp_path, 3, "late")
     assert all("ok late" in o for o, _ in outs)
     assert [p for p in os.listdir(tmp_path) if p.startswith("svo_rccl_standin_")] == []
+
+
+_OPT_IN = r'''
+import sys
+sys.path.insert(0, sys.argv[1])
+import raytracing_test_amd as rt
+try:
+    uid = rt.Exchange.unique_id()
+    print("UID", uid[:17].decode("ascii", "replace"))
+except rt.SvoError as e:
+    print("ERR", e)
+'''
+
+
+@pytest.mark.parametrize("opt_in", [False, True])
+def test_standin_needs_both_variables(tmp_path, opt_in):
+    """libsvo_rt loads another RCCL implementation only when SVO_RCCL_LIB names it AND SVO_RCCL_STANDIN=1 (ADVICE r05:
+    a stray SVO_RCCL_LIB must not turn a measurement into a stand-in run): with the variable alone the exchange's first
+    call fails with a message naming the missing opt-in; with both, the stand-in answers (its unique ids carry its
+    magic prefix).  Host only: no GPU call is made."""
+    from raytracing_test_amd import build as b
+
+    standin = b.build_rccl_standin()
+    script = tmp_path / "opt.py"
+    script.write_text(_OPT_IN)
+    env = {k: v for k, v in os.environ.items() if k not in ("SVO_RCCL_LIB", "SVO_RCCL_STANDIN")}
+    env["SVO_RCCL_LIB"] = standin
+    env["SVO_STANDIN_HOST_ONLY"] = "1"
+    if opt_in:
+        env["SVO_RCCL_STANDIN"] = "1"
+    p = subprocess.run([sys.executable, str(script), ROOT], capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    if opt_in:
+        assert "UID svo-rccl-standin:" in p.stdout, p.stdout
+    else:
+        assert "ERR" in p.stdout and "SVO_RCCL_STANDIN=1" in p.stdout, p.stdout
