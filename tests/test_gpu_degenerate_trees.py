@@ -82,3 +82,28 @@ def test_one_far_block(rt, oracle_mod, cuda):
     aimed = [((190.5, 1.5, 120.5), (1.0, 0.0, 1.0)), ((180.0, 10.0, 110.0), (1.0, -0.45, 1.0))]
     ref = _frames(rt, tree, T, "one block", steps=1000, cams=CAMS + aimed)
     assert ref["hit"].any() and (ref["pos"][ref["hit"] != 0] == [200, 1, 130]).all()
+
+
+@pytest.mark.parametrize("case", ["uniform", "one_level", "one_block"])
+def test_shade_degenerate(rt, oracle_mod, cuda, case):
+    """the shading pass on the same trees: its straight trace and the shadow rays (75 steps towards the sun, each
+    seeded from the root of the solid tree) against the oracle's shading restatement (low_res.frag's colour model)"""
+    from test_gpu_shade import _check
+
+    if case == "uniform":
+        tree, T = _pair(rt, oracle_mod, 3, [(0, 0, 0, 77)], level=1)
+        cams = CAMS
+    elif case == "one_level":
+        rng = np.random.default_rng(11)
+        pts = {tuple(p) for p in rng.integers(0, 4, (9, 3)).tolist()}
+        tree, T = _pair(rt, oracle_mod, 1, [(x, y, z, 1 + i) for i, (x, y, z) in enumerate(sorted(pts))])
+        cams = CAMS
+    else:
+        tree, T = _pair(rt, oracle_mod, 4, [(200, 1, 130, 5), (201, 1, 130, 6), (200, 2, 131, 7)])
+        cams = [((190.5, 1.5, 120.5), (1.0, 0.0, 1.0)), ((180.0, 10.0, 110.0), (1.0, -0.45, 1.0))]
+    sun = rt.sun_dir()
+    for ci, (org, d) in enumerate(cams):
+        dn = rt.normalize(d)
+        rgba, hits = tree.shade_frame(org, dn, 64, 32, 300, sun=sun, with_hits=True)
+        ref = T.shade_frame(org, dn, 64, 32, 300, sun)
+        _check(rgba, ref, rt.decode_hits(hits)["hit"], "%s cam%d" % (case, ci))
