@@ -10,7 +10,6 @@ Two such trees, full 1080p frames at the reference budget (S = 300), every field
 
 Poses: the C1 / C3 pose, the reference's default camera (globals.cpp:20-21), half-integral and
 fractional origins (the linear and segment instances)."""
-import numpy as np
 import pytest
 
 from test_gpu_parity import compare
